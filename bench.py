@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s on the RTIOW cover scene at 1920x1080x1024spp (config C2).
+
+A "step" = one full frame: every pixel of the 1920x1080 frame gets `--spp`
+camera samples (1024 by default) traced through the wavefront
+(raygen -> [extend -> shade/compact]* -> accumulate), i.e. the whole C2
+workload.  A ray = one ray segment (one closest-hit query issued by the
+integrator).  `value` = total segments / wall time over
+the timed steps (max over ranks), inputs resident in HBM.
+
+Multi-GPU (torch.distributed.run, one process per GPU): the frame is split
+into interleaved 16x16 tiles (tile t -> rank t % N, rt_render_device's
+shard arguments), each rank renders its tiles into a full-frame f64
+accumulator, and the per-rank accumulators are gathered onto rank 0 at frame
+end with one RCCL reduce over xGMI (tiles are disjoint, every other pixel is
+0.0, so the sum is the exact union).  Total work per step is fixed:
+"scaling": "strong".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "scheme-raytrace_amd"))
+
+METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector spec (FMA = 2 flops)
+# algorithmic HBM bytes of one extend launch per ray segment:
+# read ray o,d,time (7 x f64 = 56 B), write hit t (8 B) + leaf id (4 B)
+EXTEND_BYTES_PER_SEGMENT = 68
+
+
+def extend_flops_per_segment(n_sph, n_msph):
+    """Algorithmic f64 flops of the brute-force closest-hit loop per segment
+    (non-FMA count): |d|^2 = 5; sphere: oc 3 + b 5 + c 6 + disc 3 = 17;
+    moving sphere: + centre lerp 6 = 23."""
+    return 5 + 17 * n_sph + 23 * n_msph
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--spp", type=int, default=1024)
+    p.add_argument("--nx", type=int, default=1920)
+    p.add_argument("--ny", type=int, default=1080)
+    p.add_argument("--scene", default="cover")
+    p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-profile-events", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(scene, nx, ny, seed, budget_s):
+    """Time the oracle (C f64 restatement, OpenMP) on a bounded band of the
+    same frame, 1 spp, growing the band until ~budget_s of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle  # cpu_baseline leg only
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = oracle.build_scene(scene)
+    acc = np.zeros(nx * ny * 3)
+    rows, t_used, segs_total, rows_done = 4, 0.0, 0, 0
+    y0 = ny // 3
+    while t_used < budget_s and y0 + rows_done + rows <= ny:
+        lo = (y0 + rows_done) * nx
+        hi = lo + rows * nx
+        t = time.perf_counter()
+        _, segs = o.render(nx, ny, 0, 1, seed, acc, lo, hi, threads)
+        t_used += time.perf_counter() - t
+        segs_total += segs
+        rows_done += rows
+        rows *= 2
+    rate = segs_total / t_used / 1e6
+    return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": "oracle/rt_oracle.c (C f64 restatement of the Scheme hot path, OpenMP) on rows %d..%d of "
+                      "the 1920x1080 C2 frame at 1 spp (%d segments, %.1f s); Gauche (the reference runtime) "
+                      "is not installed on the box" % (y0, y0 + rows_done, segs_total, t_used)}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from rtamd import gpu, scenes
+    from rtamd._lib import call
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    nx, ny, spp = a.nx, a.ny, a.spp
+    scene = scenes.SCENES[a.scene](nx, ny)
+    ctx = gpu.default_context(local)
+    h = gpu.upload(scene, ctx)                      # one-time scene upload (not timed)
+    call("rt_set_profiling", h, 0 if a.no_profile_events else 1)
+    accum = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    lib_stream = None                               # librtamd's own stream (events live there)
+
+    def step():
+        accum.zero_()
+        torch.cuda.synchronize()
+        gpu.render_device(scene, nx, ny, 0, spp, a.seed, accum.data_ptr(), shard=rank, nshard=world,
+                          stream=lib_stream, ctx=ctx)
+        s = gpu.stats(h)
+        if world > 1:
+            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)   # RCCL gather of disjoint tiles
+        return s
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    segs = paths = 0
+    ms_ext = ms_shade = 0.0
+    launches = 0
+    for _ in range(a.steps):
+        s = step()
+        segs += s.segments
+        paths += s.paths
+        ms_ext += s.ms_extend
+        ms_shade += s.ms_shade
+        launches += s.extend_launches
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = torch.tensor([segs, paths], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    segs_all, paths_all = float(tot[0]), float(tot[1])
+    elapsed = float(tmax[0])
+    if rank == 0:
+        value = segs_all / elapsed / 1e6
+        n_sph = sum(1 for o in scene.obj_list if o.kind == "sphere")
+        n_msph = sum(1 for o in scene.obj_list if o.kind == "moving_sphere")
+        roof = None
+        valu = None
+        if launches and ms_ext > 0:
+            rays_per_launch = segs / launches
+            avg_ms = ms_ext / launches
+            achieved = EXTEND_BYTES_PER_SEGMENT * rays_per_launch / (avg_ms * 1e-3) / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    pm = json.load(f)
+                if pm.get("scene") == a.scene and pm.get("bytes_per_segment"):
+                    traffic = round(pm["bytes_per_segment"] * rays_per_launch)
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "kernel": "k_extend", "bytes_per_launch": round(EXTEND_BYTES_PER_SEGMENT * rays_per_launch),
+                    "avg_launch_ms": round(avg_ms, 4)}
+            fl = extend_flops_per_segment(n_sph, n_msph)
+            tf = fl * rays_per_launch / (avg_ms * 1e-3) / 1e12
+            valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4), "flops_per_segment": fl}
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: RTIOW cover scene (random-scene, main.scm:31-89 + repairs R1/R3) generated "
+                    "from host seed 0x5EED0001; path RNG seed %#x" % a.seed,
+            "config": {"workload": "C2: %s scene %dx%dx%dspp, one full frame per step" % (a.scene, nx, ny, spp),
+                       "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
+                       "parallelism": "tile-shard%d" % world if world > 1 else "single"},
+            "roofline": roof, "valu": valu,
+            "samples_per_s": round(paths_all / elapsed, 1),
+            "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
+            "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, nx, ny, a.seed, a.cpu_baseline_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/*
+ * rt.h — C ABI of the MI355X wavefront path tracer (librtamd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: the per-pixel
+ * `trace-all` → recursive `color` loop of soma-arc/scheme-raytrace
+ * (main.scm:100-121, 471-491) and everything it calls through the
+ * closure-vector protocol (geometry.scm:14-15, material.scm:15-22,
+ * texture.scm:9-10).  Scheme closures are opaque to C, so the drop-in keeps
+ * the reference's *constructor* names and arities and has each constructor
+ * append a typed descriptor to a scene builder.
+ *
+ * Conventions
+ *   - every entry point returns an int status: 0 = ok, nonzero = error, with
+ *     a thread-local message from rt_last_error();
+ *   - handles (contexts, scenes, object/material/texture ids) are ints;
+ *   - the caller owns every host buffer; the library copies descriptors at
+ *     commit time and owns all device memory it allocates;
+ *   - vectors are `const double v[3]` (the reference's f64vector vec3,
+ *     vec.scm:7);
+ *   - one host thread per context (the reference renders on one thread,
+ *     main.scm:633-634); multi-GPU = one process per GPU.
+ *   - arithmetic is f64 throughout, as in the reference (Gauche flonums).
+ */
+#ifndef RTAMD_RT_H
+#define RTAMD_RT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
+ * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
+ * black (main.scm:97-98). */
+enum { RT_SKY_GRADIENT = 0, RT_SKY_BLACK = 1 };
+
+/* Axis-aligned rect planes (geometry.scm:376-431). */
+enum { RT_RECT_XY = 0, RT_RECT_XZ = 1, RT_RECT_YZ = 2 };
+
+/* Number of doubles in a camera vector: the reference's 10-slot camera
+ * (camera.scm:33-78) flattened = llc(3) horizontal(3) vertical(3) origin(3)
+ * w(3) u(3) v(3) lens-radius time0 time1. */
+#define RT_CAMERA_DOUBLES 24
+
+/* ---- library / context ------------------------------------------------ */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* out_count);
+/* Context on one HIP device; owns a HIP stream and all device memory. */
+int rt_context_create(int device, int* out_ctx);
+int rt_context_destroy(int ctx);
+
+/* ---- scene building (replaces the closure-vector constructors) ---------- */
+int rt_scene_begin(int ctx, int* out_scene);
+int rt_scene_destroy(int scene);
+
+/* textures — texture.scm:12-34 */
+int rt_add_texture_constant(int scene, const double rgb[3], int* out_tex);     /* t:constant-texture :12 */
+int rt_add_texture_checker(int scene, int even_tex, int odd_tex, int* out_tex); /* t:checker-texture :16 */
+int rt_add_texture_noise(int scene, double scale, int* out_tex);               /* t:noise-texture :25 */
+int rt_add_texture_marble(int scene, double scale, int* out_tex);              /* t:marble-texture :30 */
+
+/* materials — material.scm:24-111 */
+int rt_add_material_lambertian(int scene, int albedo_tex, int* out_mat);            /* m:make-lambertian :24 */
+int rt_add_material_metal(int scene, int albedo_tex, double fuzz, int* out_mat);    /* m:make-metal :45 */
+int rt_add_material_dielectric(int scene, double ref_idx, int* out_mat);            /* m:make-dielectric :76 */
+int rt_add_material_diffuse_light(int scene, int emit_tex, int* out_mat);           /* m:make-diffuse-light :103 */
+
+/* hitables — geometry.scm / bezier.scm.  Objects may be shared and nested. */
+int rt_add_sphere(int scene, const double center[3], double radius, int mat, int* out_obj);   /* g:make-sphere :146 */
+int rt_add_moving_sphere(int scene, const double center0[3], const double center1[3],
+                         double time0, double time1, double radius, int mat, int* out_obj);     /* g:make-moving-sphere :177 */
+/* axis: RT_RECT_XY (a=x,b=y,k=z), RT_RECT_XZ (a=x,b=z,k=y), RT_RECT_YZ (a=y,b=z,k=x) */
+int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1, double k,
+                int mat, int* out_obj);                                                          /* g:make-{xy,xz,yz}-rect :376-431 */
+int rt_add_flip_normals(int scene, int obj, int* out_obj);                                       /* g:flip-normals :433 */
+int rt_add_box(int scene, const double p0[3], const double p1[3], int mat, int* out_obj);       /* g:make-box :444 */
+int rt_add_translate(int scene, int obj, const double offset[3], int* out_obj);                 /* g:translate :465 */
+int rt_add_rotate_y(int scene, int obj, double angle_deg, int* out_obj);                        /* g:rotate-y :483 */
+/* An object list (make-scene's obj-list, geometry.scm:52; a nested list). */
+int rt_add_list(int scene, const int* objs, int n, int* out_obj);
+/* g:make-bvh-node :226 / g:make-bvh-with-sah :294.  Closest-hit over the
+ * children; the library builds its own acceleration structure. */
+int rt_add_bvh(int scene, const int* objs, int n, double time0, double time1, int sah, int* out_obj);
+
+/* camera — cam:make-camera (camera.scm:63-78) evaluated on the host side;
+ * the 24 doubles are the 10 slots the reference's get-ray reads. */
+int rt_make_camera(const double lookfrom[3], const double lookat[3], const double vup[3],
+                   double vfov_deg, double aspect, double aperture, double focus_dist,
+                   double time0, double time1, double out_cam[RT_CAMERA_DOUBLES]);
+int rt_set_camera(int scene, const double cam[RT_CAMERA_DOUBLES]);
+int rt_set_sky(int scene, int sky);
+/* Perlin tables (perlin.scm:32-36): the reference draws them from the global
+ * RNG at module load; here they are data.  ranvec: 256 unit vec3, perm: 256
+ * entries each (a permutation of 0..255). */
+int rt_set_perlin_tables(int scene, const double ranvec[256 * 3], const int32_t perm_x[256],
+                         const int32_t perm_y[256], const int32_t perm_z[256]);
+/* Fix the world (make-scene's obj-list) and upload the scene to the device. */
+int rt_scene_commit(int scene, int world_list_obj);
+
+/* ---- rendering -------------------------------------------------------- */
+/* One call = `spp_count` successive trace-all passes (main.scm:471-491) with
+ * pass indices spp_begin+1 .. spp_begin+spp_count: for every pixel j = y*nx+x
+ * (y = 0 is the bottom row) the per-sample colours are added to accum[3j..3j+2]
+ * in sample order, exactly the `*raw-data*` running sum.  Random numbers come
+ * from a counter-based stream keyed by (seed, pixel, sample), so results do
+ * not depend on launch geometry, batching or sharding.
+ *
+ * rt_render: accum is a caller-owned HOST buffer (nx*ny*3 doubles), copied to
+ * the device and back (PCIe-inclusive).
+ * rt_render_device: accum is caller-owned DEVICE memory on the context's GPU
+ * (e.g. a torch tensor's data_ptr); stream is a hipStream_t or NULL for the
+ * context's own stream.  shard_index/shard_count select an interleaved subset
+ * of 16x16 pixel tiles (tile t belongs to shard t % shard_count); pixels of
+ * other shards are left untouched. */
+int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
+              double* accum_host);
+int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
+                     int shard_index, int shard_count, double* accum_device, void* stream);
+
+/* Statistics of the last render on this scene. */
+typedef struct rt_stats {
+    uint64_t segments;    /* closest-hit queries issued by the integrator (ray segments) */
+    uint64_t paths;       /* camera samples */
+    double   ms_total;    /* wall time of the render call */
+    double   ms_extend;   /* summed device time of the extend (closest-hit) kernel */
+    double   ms_shade;    /* summed device time of the shade kernel */
+    uint64_t extend_launches;
+    uint64_t extend_rays; /* = segments */
+    uint32_t max_depth_seen;
+    uint32_t reserved;
+} rt_stats;
+int rt_get_stats(int scene, rt_stats* out);
+/* Record per-kernel HIP events during renders (adds a little host overhead). */
+int rt_set_profiling(int scene, int enabled);
+
+/* Resolve (main.scm:481-491): c = sqrt(sum/sample_count) per channel, then
+ * floor(255.99*min(1,c)) into out (nx*ny*3 bytes, same y-up layout). Host. */
+int rt_resolve_u8(const double* accum, int nx, int ny, int sample_count, uint8_t* out);
+/* Same on the device (accum_device and out_device are device pointers). */
+int rt_resolve_u8_device(int ctx, const double* accum_device, int nx, int ny, int sample_count,
+                         uint8_t* out_device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTAMD_RT_H */

@@ -1,0 +1,685 @@
+/*
+ * rt_oracle.c — CPU f64 restatement of the reference hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the timed CPU baseline) — never as part of the product path.
+ *
+ * It restates, in the reference's own evaluation order, the Gauche Scheme code
+ * of soma-arc/scheme-raytrace (reference @ /root/reference):
+ *   vec.scm:7-70           vector algebra (left folds; unit = v * (1/|v|))
+ *   ray.scm:8-54           ray #(o d time), make-ray forces time 0 (Q4)
+ *   util.scm:9-23,37-44    rejection samplers, cosine direction (x2 quirk, Q1)
+ *   onb.scm:8-36           ONB from w, `local`
+ *   camera.scm:63-92       make-camera, get-ray (direction not normalised)
+ *   geometry.scm:14-56     hit dispatch, hit-obj-list (closest, strict <)
+ *   geometry.scm:146-215   sphere / moving sphere
+ *   geometry.scm:376-543   rects, flip-normals, box, translate, rotate-y
+ *   material.scm:15-111    lambertian / metal / dielectric / diffuse light
+ *   texture.scm:12-34      constant / checker / noise / marble
+ *   perlin.scm:51-103      perlin-interp, noise (aliasing quirk Q2), turb
+ *   main.scm:91-124        sky-color, black, color (recursive), correct-gamma
+ *   main.scm:471-491       trace-all (jitter, running sum, resolve)
+ * with the repairs R1-R3 of SURVEY.md Appendix A (metal / dielectric are
+ * specular: L = e + att*L_next).  The reference's global srfi-27 stream is
+ * replaced by the counter-based Philox4x32-10 stream keyed by
+ * (seed, pixel, sample) that the GPU uses too, with
+ * draws consumed in the order the Scheme code consumes them (arguments
+ * evaluated left to right).
+ *
+ * Build: see oracle/Makefile (-O2 -ffp-contract=off: no FMA contraction, so
+ * every f64 operation rounds exactly as the reference's flonum ops do).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+#define ORC_MAX_DEPTH 100              /* main.scm:26 */
+#define ORC_TMIN 0.001                 /* main.scm:104 */
+#define ORC_TMAX 999999999999.0        /* constant.scm:6 */
+#define ORC_PI 3.141592653589793       /* math.const pi = 4*atan(1) */
+
+/* ------------------------------------------------------------------ RNG */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants). */
+static void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ ctr[1] ^ k0, n2 = hi0 ^ ctr[3] ^ k1;
+        ctr[0] = n0; ctr[1] = lo1; ctr[2] = n2; ctr[3] = lo0;
+    }
+}
+
+void orc_philox(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+    uint32_t c[4] = {ctr_in[0], ctr_in[1], ctr_in[2], ctr_in[3]};
+    philox4x32_10(c, k0, k1);
+    memcpy(out, c, sizeof c);
+}
+
+/* two u32 -> double in (0,1): 52 random bits, u = (2k+1) * 2^-53 */
+static double u32pair_to_unit(uint32_t hi, uint32_t lo) {
+    uint64_t k = ((uint64_t)(hi >> 12) << 32) | lo;
+    return (double)(2 * k + 1) * (1.0 / 9007199254740992.0);
+}
+
+typedef struct {
+    uint32_t k0, k1, pix, smp, ctr;
+} orc_rng;
+
+/* draw d of the stream: block d>>1, ctr = {block, sample, pixel, 0} */
+static double orc_random_real(orc_rng* g) {
+    uint32_t d = g->ctr++;
+    uint32_t c[4] = {d >> 1, g->smp, g->pix, 0u};
+    philox4x32_10(c, g->k0, g->k1);
+    return (d & 1u) ? u32pair_to_unit(c[2], c[3]) : u32pair_to_unit(c[0], c[1]);
+}
+
+/* exported for tests: draw `n` values of stream (seed, pix, smp) from draw index `first` */
+void orc_stream(uint64_t seed, uint32_t pix, uint32_t smp, uint32_t first, int n, double* out) {
+    orc_rng g = {(uint32_t)seed, (uint32_t)(seed >> 32), pix, smp, first};
+    for (int i = 0; i < n; ++i) out[i] = orc_random_real(&g);
+}
+
+/* --------------------------------------------------------------- vec.scm */
+typedef struct { double x, y, z; } v3;
+static inline v3 V(double x, double y, double z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+/* sum / diff are left folds of f64vector-add / -sub (vec.scm:20-33) */
+static inline v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 vscale(v3 a, double k) { return V(a.x * k, a.y * k, a.z * k); }
+/* f64vector-dot: r = 0; r += a_i*b_i (i = 0..2) */
+static inline double vdot(v3 a, v3 b) {
+    double r = 0.0;
+    r += a.x * b.x; r += a.y * b.y; r += a.z * b.z;
+    return r;
+}
+static inline double vlength(v3 a) { return sqrt(vdot(a, a)); }          /* vec.scm:54 */
+static inline v3 vunit(v3 a) { double k = 1.0 / vlength(a); return vscale(a, k); } /* :60-62 */
+static inline v3 vcross(v3 a, v3 b) {                                       /* :64-70 */
+    return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+
+typedef struct { v3 o, d; double time; } ray_t;
+static inline v3 point_at(ray_t r, double t) { return vadd(r.o, vscale(r.d, t)); } /* ray.scm:23-25 */
+
+/* ------------------------------------------------------------- scene data */
+enum { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
+enum { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
+enum { OBJ_SPHERE = 0, OBJ_MOVING_SPHERE, OBJ_RECT, OBJ_FLIP, OBJ_BOX, OBJ_TRANSLATE,
+       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH };
+
+typedef struct { int type, a, b; v3 rgb; double scale; } orc_tex;
+typedef struct { int type, tex; double fuzz, ref_idx; } orc_mat;
+typedef struct {
+    int type, mat, child, axis;
+    int first, count;                   /* OBJ_LIST / OBJ_BVH children in kids[] */
+    v3 c0, c1;                          /* sphere centre / moving centres / box p0,p1 / offset */
+    double r, t0, t1;
+    double a0, a1, b0, b1, k;           /* rect */
+    double sin_t, cos_t;                /* rotate-y */
+    int box_list;                       /* OBJ_BOX: its 6-rect list object */
+} orc_obj;
+
+typedef struct {
+    orc_tex* tex; int ntex, ctex;
+    orc_mat* mat; int nmat, cmat;
+    orc_obj* obj; int nobj, cobj;
+    int* kids; int nkids, ckids;
+    double cam[24];
+    int sky, world;
+    v3 ranvec[256];
+    int perm_x[256], perm_y[256], perm_z[256];
+    int have_perlin;
+} orc_scene;
+
+#define GROW(ptr, n, cap)                                                    \
+    do {                                                                     \
+        if ((n) >= (cap)) {                                                  \
+            (cap) = (cap) ? 2 * (cap) : 16;                                  \
+            (ptr) = realloc((ptr), (size_t)(cap) * sizeof(*(ptr)));          \
+        }                                                                    \
+    } while (0)
+
+orc_scene* orc_scene_new(void) {
+    orc_scene* s = calloc(1, sizeof *s);
+    s->world = -1;
+    return s;
+}
+void orc_scene_free(orc_scene* s) {
+    if (!s) return;
+    free(s->tex); free(s->mat); free(s->obj); free(s->kids); free(s);
+}
+
+int orc_add_texture_constant(orc_scene* s, const double rgb[3]) {
+    GROW(s->tex, s->ntex, s->ctex);
+    orc_tex t; memset(&t, 0, sizeof t); t.type = TEX_CONSTANT; t.rgb = V(rgb[0], rgb[1], rgb[2]);
+    s->tex[s->ntex] = t; return s->ntex++;
+}
+int orc_add_texture_checker(orc_scene* s, int even, int odd) {
+    GROW(s->tex, s->ntex, s->ctex);
+    orc_tex t; memset(&t, 0, sizeof t); t.type = TEX_CHECKER; t.a = even; t.b = odd;
+    s->tex[s->ntex] = t; return s->ntex++;
+}
+int orc_add_texture_noise(orc_scene* s, double sc) {
+    GROW(s->tex, s->ntex, s->ctex);
+    orc_tex t; memset(&t, 0, sizeof t); t.type = TEX_NOISE; t.scale = sc;
+    s->tex[s->ntex] = t; return s->ntex++;
+}
+int orc_add_texture_marble(orc_scene* s, double sc) {
+    GROW(s->tex, s->ntex, s->ctex);
+    orc_tex t; memset(&t, 0, sizeof t); t.type = TEX_MARBLE; t.scale = sc;
+    s->tex[s->ntex] = t; return s->ntex++;
+}
+static int add_mat(orc_scene* s, int type, int tex, double fuzz, double ref) {
+    GROW(s->mat, s->nmat, s->cmat);
+    orc_mat m; m.type = type; m.tex = tex; m.fuzz = fuzz; m.ref_idx = ref;
+    s->mat[s->nmat] = m; return s->nmat++;
+}
+int orc_add_material_lambertian(orc_scene* s, int tex) { return add_mat(s, MAT_LAMBERTIAN, tex, 0, 0); }
+int orc_add_material_metal(orc_scene* s, int tex, double fuzz) { return add_mat(s, MAT_METAL, tex, fuzz, 0); }
+int orc_add_material_dielectric(orc_scene* s, double ref) { return add_mat(s, MAT_DIELECTRIC, -1, 0, ref); }
+int orc_add_material_diffuse_light(orc_scene* s, int tex) { return add_mat(s, MAT_DIFFUSE_LIGHT, tex, 0, 0); }
+
+static int new_obj(orc_scene* s, int type) {
+    GROW(s->obj, s->nobj, s->cobj);
+    memset(&s->obj[s->nobj], 0, sizeof(orc_obj));
+    s->obj[s->nobj].type = type;
+    s->obj[s->nobj].child = -1;
+    s->obj[s->nobj].mat = -1;
+    return s->nobj++;
+}
+int orc_add_sphere(orc_scene* s, const double c[3], double r, int mat) {
+    int i = new_obj(s, OBJ_SPHERE);
+    s->obj[i].c0 = V(c[0], c[1], c[2]); s->obj[i].r = r; s->obj[i].mat = mat;
+    return i;
+}
+int orc_add_moving_sphere(orc_scene* s, const double c0[3], const double c1[3], double t0, double t1,
+                          double r, int mat) {
+    int i = new_obj(s, OBJ_MOVING_SPHERE);
+    orc_obj* o = &s->obj[i];
+    o->c0 = V(c0[0], c0[1], c0[2]); o->c1 = V(c1[0], c1[1], c1[2]);
+    o->t0 = t0; o->t1 = t1; o->r = r; o->mat = mat;
+    return i;
+}
+int orc_add_rect(orc_scene* s, int axis, double a0, double a1, double b0, double b1, double k, int mat) {
+    int i = new_obj(s, OBJ_RECT);
+    orc_obj* o = &s->obj[i];
+    o->axis = axis; o->a0 = a0; o->a1 = a1; o->b0 = b0; o->b1 = b1; o->k = k; o->mat = mat;
+    return i;
+}
+int orc_add_flip_normals(orc_scene* s, int child) {
+    int i = new_obj(s, OBJ_FLIP);
+    s->obj[i].child = child; s->obj[i].mat = s->obj[child].mat;
+    return i;
+}
+int orc_add_list(orc_scene* s, const int* objs, int n) {
+    int i = new_obj(s, OBJ_LIST);
+    s->obj[i].first = s->nkids; s->obj[i].count = n;
+    for (int j = 0; j < n; ++j) { GROW(s->kids, s->nkids, s->ckids); s->kids[s->nkids++] = objs[j]; }
+    return i;
+}
+int orc_add_bvh(orc_scene* s, const int* objs, int n, double t0, double t1, int sah) {
+    (void)t0; (void)t1; (void)sah;
+    int i = orc_add_list(s, objs, n);
+    s->obj[i].type = OBJ_BVH;
+    return i;
+}
+/* geometry.scm:444-463: the box is a scene of 6 rects (in this order) */
+int orc_add_box(orc_scene* s, const double p0[3], const double p1[3], int mat) {
+    int r[6];
+    r[0] = orc_add_rect(s, 0, p0[0], p1[0], p0[1], p1[1], p1[2], mat);
+    r[1] = orc_add_flip_normals(s, orc_add_rect(s, 0, p0[0], p1[0], p0[1], p1[1], p0[2], mat));
+    r[2] = orc_add_rect(s, 1, p0[0], p1[0], p0[2], p1[2], p1[1], mat);
+    r[3] = orc_add_flip_normals(s, orc_add_rect(s, 1, p0[0], p1[0], p0[2], p1[2], p0[1], mat));
+    r[4] = orc_add_rect(s, 2, p0[1], p1[1], p0[2], p1[2], p1[0], mat);
+    r[5] = orc_add_flip_normals(s, orc_add_rect(s, 2, p0[1], p1[1], p0[2], p1[2], p0[0], mat));
+    int lst = orc_add_list(s, r, 6);
+    int i = new_obj(s, OBJ_BOX);
+    s->obj[i].box_list = lst; s->obj[i].mat = mat;
+    s->obj[i].c0 = V(p0[0], p0[1], p0[2]); s->obj[i].c1 = V(p1[0], p1[1], p1[2]);
+    return i;
+}
+int orc_add_translate(orc_scene* s, int child, const double off[3]) {
+    int i = new_obj(s, OBJ_TRANSLATE);
+    s->obj[i].child = child; s->obj[i].c0 = V(off[0], off[1], off[2]);
+    s->obj[i].mat = s->obj[child].mat;
+    return i;
+}
+/* geometry.scm:483-487: radians = pi/180 * angle */
+int orc_add_rotate_y(orc_scene* s, int child, double angle) {
+    int i = new_obj(s, OBJ_ROTATE_Y);
+    double radians = (ORC_PI / 180.0) * angle;
+    s->obj[i].child = child; s->obj[i].sin_t = sin(radians); s->obj[i].cos_t = cos(radians);
+    s->obj[i].mat = s->obj[child].mat;
+    return i;
+}
+void orc_set_camera(orc_scene* s, const double cam[24]) { memcpy(s->cam, cam, sizeof s->cam); }
+void orc_set_sky(orc_scene* s, int sky) { s->sky = sky; }
+void orc_set_world(orc_scene* s, int world) { s->world = world; }
+void orc_set_perlin_tables(orc_scene* s, const double* ranvec, const int32_t* px, const int32_t* py,
+                           const int32_t* pz) {
+    for (int i = 0; i < 256; ++i) {
+        s->ranvec[i] = V(ranvec[3 * i], ranvec[3 * i + 1], ranvec[3 * i + 2]);
+        s->perm_x[i] = px[i]; s->perm_y[i] = py[i]; s->perm_z[i] = pz[i];
+    }
+    s->have_perlin = 1;
+}
+
+/* camera.scm:63-78 — make-camera */
+void orc_make_camera(const double from[3], const double at[3], const double vup_[3], double vfov,
+                     double aspect, double aperture, double focus, double t0, double t1, double out[24]) {
+    v3 lookfrom = V(from[0], from[1], from[2]), lookat = V(at[0], at[1], at[2]);
+    v3 vup = V(vup_[0], vup_[1], vup_[2]);
+    double theta = vfov * (ORC_PI / 180.0);
+    double half_height = tan(theta / 2);
+    double half_width = aspect * half_height;
+    v3 w = vunit(vsub(lookfrom, lookat));
+    v3 u = vunit(vcross(vup, w));
+    v3 v = vcross(w, u);
+    v3 llc = vsub(vsub(vsub(lookfrom, vscale(u, half_width * focus)), vscale(v, half_height * focus)),
+                  vscale(w, focus));
+    v3 hor = vscale(u, 2 * half_width * focus);
+    v3 ver = vscale(v, 2 * half_height * focus);
+    v3 slots[7] = {llc, hor, ver, lookfrom, w, u, v};
+    for (int i = 0; i < 7; ++i) { out[3 * i] = slots[i].x; out[3 * i + 1] = slots[i].y; out[3 * i + 2] = slots[i].z; }
+    out[21] = aperture / 2; out[22] = t0; out[23] = t1;
+}
+
+/* ---------------------------------------------------------- util / onb */
+/* util.scm:9-15 */
+static v3 random_in_unit_sphere(orc_rng* g) {
+    for (;;) {
+        double a = orc_random_real(g), b = orc_random_real(g), c = orc_random_real(g);
+        v3 p = vsub(vscale(V(a, b, c), 2), V(1, 1, 1));
+        if (vdot(p, p) < 1) return p;
+    }
+}
+/* util.scm:17-23 */
+static v3 random_in_unit_disk(orc_rng* g) {
+    for (;;) {
+        double a = orc_random_real(g), b = orc_random_real(g);
+        v3 p = vsub(vscale(V(a, b, 0), 2), V(1, 1, 0));
+        if (vdot(p, p) < 1) return p;
+    }
+}
+/* util.scm:37-44 — note the stray *2 on x and y (Q1) */
+static v3 random_cosine_direction(orc_rng* g) {
+    double r1 = orc_random_real(g);
+    double r2 = orc_random_real(g);
+    double z = sqrt(1 - r2);
+    double phi = 2 * ORC_PI * r1;
+    double x = cos(phi) * 2 * sqrt(r2);
+    double y = sin(phi) * 2 * sqrt(r2);
+    return V(x, y, z);
+}
+typedef struct { v3 u, v, w; } onb_t;
+static onb_t make_onb_from_w(v3 n) {                                   /* onb.scm:8-16 */
+    onb_t b;
+    v3 axis2 = vunit(n);
+    v3 a = (fabs(axis2.x) > 0.9) ? V(0, 1, 0) : V(1, 0, 0);
+    v3 axis1 = vunit(vcross(axis2, a));
+    v3 axis0 = vcross(axis2, axis1);
+    b.u = axis0; b.v = axis1; b.w = axis2;
+    return b;
+}
+static v3 onb_local(onb_t b, v3 a) {                                   /* onb.scm:27-36 */
+    return vadd(vadd(vscale(b.u, a.x), vscale(b.v, a.y)), vscale(b.w, a.z));
+}
+
+/* ----------------------------------------------------------- perlin.scm */
+static double perlin_noise(const orc_scene* s, v3 p) {
+    double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    long i = (long)fx, j = (long)fy, k = (long)fz;
+    /* perlin.scm:76 — (make-vector 2 (make-vector 2 (make-vector 2))) shares
+     * one innermost vector, so after the fill loop c[*][*][dk] holds the
+     * value written at di = dj = 1 (Q2). */
+    v3 c[2];
+    for (int dk = 0; dk < 2; ++dk) {
+        int h = s->perm_x[(i + 1) & 255] ^ s->perm_y[(j + 1) & 255] ^ s->perm_z[(k + dk) & 255];
+        c[dk] = s->ranvec[h];
+    }
+    /* perlin-interp :51-67 */
+    double uu = u * u * (3 - 2 * u);
+    double vv = v * v * (3 - 2 * v);
+    double ww = w * w * (3 - 2 * w);
+    double acc = 0;
+    for (int di = 0; di < 2; ++di)
+        for (int dj = 0; dj < 2; ++dj)
+            for (int dk = 0; dk < 2; ++dk) {
+                double wi = di ? uu : (1 - uu);
+                double wj = dj ? vv : (1 - vv);
+                double wk = dk ? ww : (1 - ww);
+                v3 weight = V(u - di, v - dj, w - dk);
+                acc += wi * wj * wk * vdot(weight, c[dk]);
+            }
+    return acc;
+}
+static double perlin_turb(const orc_scene* s, v3 p) {                  /* perlin.scm:92-103 */
+    double acc = 0, weight = 1;
+    for (int depth = 0; depth < 7; ++depth) {
+        acc = acc + weight * perlin_noise(s, p);
+        p = vscale(p, 2);
+        weight = weight * 0.5;
+    }
+    return fabs(acc);
+}
+
+/* ---------------------------------------------------------- texture.scm */
+static v3 tex_value(const orc_scene* s, int id, double u, double v, v3 p) {
+    const orc_tex* t = &s->tex[id];
+    switch (t->type) {
+    case TEX_CONSTANT: return t->rgb;
+    case TEX_CHECKER: {                                                 /* :16-23 */
+        double sines = sin(10 * p.x) * sin(10 * p.y) * sin(10 * p.z);
+        return (sines < 0) ? tex_value(s, t->b, u, v, p) : tex_value(s, t->a, u, v, p);
+    }
+    case TEX_NOISE:                                                     /* :25-28 */
+        return vscale(V(1, 1, 1), perlin_noise(s, vscale(p, t->scale)));
+    case TEX_MARBLE: {                                                  /* :30-34 */
+        double m = 0.5 * (1 + sin(t->scale * p.z + 10 * perlin_turb(s, p)));
+        return vscale(V(1, 1, 1), m);
+    }
+    }
+    return V(0, 0, 0);
+}
+
+/* --------------------------------------------------------- geometry.scm */
+typedef struct { double t; v3 p, n; int mat; double u, v; } hitrec;
+
+static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec);
+
+static int hit_list(const orc_scene* s, int first, int count, ray_t r, double tmin, double tmax,
+                    hitrec* rec) {                                      /* :33-50 */
+    int hit_anything = 0;
+    double closest = tmax;
+    hitrec tmp;
+    for (int i = 0; i < count; ++i) {
+        if (hit_obj(s, s->kids[first + i], r, tmin, closest, &tmp)) {
+            hit_anything = 1; closest = tmp.t; *rec = tmp;
+        }
+    }
+    return hit_anything;
+}
+
+static int sphere_hit(v3 center, double radius, int mat, ray_t r, double tmin, double tmax, hitrec* rec) {
+    v3 oc = vsub(r.o, center);
+    double a = vdot(r.d, r.d);
+    double b = vdot(oc, r.d);
+    double c = vdot(oc, oc) - radius * radius;
+    double disc = b * b - a * c;
+    if (disc <= 0) return 0;
+    double temp = (-b - sqrt(disc)) / a;
+    if (!(tmin < temp && temp < tmax)) {
+        temp = (-b + sqrt(disc)) / a;
+        if (!(tmin < temp && temp < tmax)) return 0;
+    }
+    rec->t = temp;
+    rec->p = point_at(r, temp);
+    rec->n = vscale(vsub(rec->p, center), 1.0 / radius);
+    rec->mat = mat;
+    /* get-sphere-uv (:138-144) is dead for every reference texture (Q3) */
+    rec->u = 0; rec->v = 0;
+    return 1;
+}
+
+static int rect_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitrec* rec) {
+    /* axis 0: xy (k on z), 1: xz (k on y), 2: yz (k on x) — :376-431 */
+    double ok, dk, oa, da, ob, db;
+    v3 n;
+    if (o->axis == 0) { ok = r.o.z; dk = r.d.z; oa = r.o.x; da = r.d.x; ob = r.o.y; db = r.d.y; n = V(0, 0, 1); }
+    else if (o->axis == 1) { ok = r.o.y; dk = r.d.y; oa = r.o.x; da = r.d.x; ob = r.o.z; db = r.d.z; n = V(0, 1, 0); }
+    else { ok = r.o.x; dk = r.d.x; oa = r.o.y; da = r.d.y; ob = r.o.z; db = r.d.z; n = V(1, 0, 0); }
+    double t = (o->k - ok) / dk;
+    if (t < tmin || t > tmax) return 0;
+    double a = oa + t * da;
+    double b = ob + t * db;
+    if (a < o->a0 || a > o->a1 || b < o->b0 || b > o->b1) return 0;
+    rec->t = t;
+    rec->p = point_at(r, t);
+    rec->n = n;
+    rec->mat = o->mat;
+    rec->u = (a - o->a0) / (o->a1 - o->a0);
+    rec->v = (b - o->b0) / (o->b1 - o->b0);
+    return 1;
+}
+
+static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec) {
+    const orc_obj* o = &s->obj[id];
+    switch (o->type) {
+    case OBJ_SPHERE: return sphere_hit(o->c0, o->r, o->mat, r, tmin, tmax, rec);
+    case OBJ_MOVING_SPHERE: {                                           /* :177-208 */
+        v3 center = vadd(o->c0, vscale(vsub(o->c1, o->c0), (r.time - o->t0) / (o->t1 - o->t0)));
+        return sphere_hit(center, o->r, o->mat, r, tmin, tmax, rec);
+    }
+    case OBJ_RECT: return rect_hit(o, r, tmin, tmax, rec);
+    case OBJ_FLIP:                                                      /* :433-442 */
+        if (!hit_obj(s, o->child, r, tmin, tmax, rec)) return 0;
+        rec->n = vscale(rec->n, -1);
+        return 1;
+    case OBJ_BOX: {                                                     /* :444-463 */
+        const orc_obj* l = &s->obj[o->box_list];
+        return hit_list(s, l->first, l->count, r, tmin, tmax, rec);
+    }
+    case OBJ_TRANSLATE: {                                               /* :465-481 */
+        ray_t moved = {vsub(r.o, o->c0), r.d, r.time};
+        if (!hit_obj(s, o->child, moved, tmin, tmax, rec)) return 0;
+        rec->p = vadd(rec->p, o->c0);
+        return 1;
+    }
+    case OBJ_ROTATE_Y: {                                                /* :511-540 */
+        double sn = o->sin_t, cs = o->cos_t;
+        ray_t rr;
+        rr.o = V(cs * r.o.x - sn * r.o.z, r.o.y, sn * r.o.x + cs * r.o.z);
+        rr.d = V(cs * r.d.x - sn * r.d.z, r.d.y, sn * r.d.x + cs * r.d.z);
+        rr.time = r.time;
+        if (!hit_obj(s, o->child, rr, tmin, tmax, rec)) return 0;
+        v3 p = V(cs * rec->p.x + sn * rec->p.z, rec->p.y, (-sn) * rec->p.x + cs * rec->p.z);
+        v3 n = V(cs * rec->n.x + sn * rec->n.z, rec->n.y, (-sn) * rec->n.x + cs * rec->n.z);
+        rec->p = p; rec->n = n; rec->mat = o->mat;
+        return 1;
+    }
+    case OBJ_LIST:
+    case OBJ_BVH:
+        return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------- material.scm */
+static v3 reflect(v3 v, v3 n) { return vsub(v, vscale(n, 2 * vdot(v, n))); }  /* :41-43 */
+static double schlick(double cosine, double ref_idx) {                         /* :69-74 */
+    double r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * pow(1 - cosine, 5);
+}
+static int refract(v3 v, v3 n, double ni_over_nt, v3* out) {                   /* :59-67 */
+    v3 uv = vunit(v);
+    double dt = vdot(uv, n);
+    double disc = 1 - ni_over_nt * ni_over_nt * (1 - dt * dt);
+    if (disc > 0) {
+        *out = vsub(vscale(vsub(v, vscale(n, dt)), ni_over_nt), vscale(n, sqrt(disc)));
+        return 1;
+    }
+    return 0;
+}
+
+/* exported KAT helpers */
+double orc_schlick(double c, double r) { return schlick(c, r); }
+int orc_refract(const double v[3], const double n[3], double ni, double out[3]) {
+    v3 o;
+    int ok = refract(V(v[0], v[1], v[2]), V(n[0], n[1], n[2]), ni, &o);
+    if (ok) { out[0] = o.x; out[1] = o.y; out[2] = o.z; }
+    return ok;
+}
+void orc_reflect(const double v[3], const double n[3], double out[3]) {
+    v3 o = reflect(V(v[0], v[1], v[2]), V(n[0], n[1], n[2]));
+    out[0] = o.x; out[1] = o.y; out[2] = o.z;
+}
+double orc_noise(const orc_scene* s, const double p[3]) { return perlin_noise(s, V(p[0], p[1], p[2])); }
+double orc_turb(const orc_scene* s, const double p[3]) { return perlin_turb(s, V(p[0], p[1], p[2])); }
+void orc_tex_value(const orc_scene* s, int tex, const double p[3], double out[3]) {
+    v3 c = tex_value(s, tex, 0, 0, V(p[0], p[1], p[2]));
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+}
+void orc_onb(const double n[3], double out[9]) {
+    onb_t b = make_onb_from_w(V(n[0], n[1], n[2]));
+    out[0] = b.u.x; out[1] = b.u.y; out[2] = b.u.z;
+    out[3] = b.v.x; out[4] = b.v.y; out[5] = b.v.z;
+    out[6] = b.w.x; out[7] = b.w.y; out[8] = b.w.z;
+}
+/* closest hit of the world list: returns 1 on hit, rec = {t, p(3), n(3), mat} */
+int orc_hit_world(const orc_scene* s, const double o[3], const double d[3], double time, double out[8]) {
+    ray_t r = {V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), time};
+    hitrec rec;
+    const orc_obj* w = &s->obj[s->world];
+    if (!hit_list(s, w->first, w->count, r, ORC_TMIN, ORC_TMAX, &rec)) return 0;
+    out[0] = rec.t; out[1] = rec.p.x; out[2] = rec.p.y; out[3] = rec.p.z;
+    out[4] = rec.n.x; out[5] = rec.n.y; out[6] = rec.n.z; out[7] = rec.mat;
+    return 1;
+}
+
+/* -------------------------------------------------------------- main.scm */
+static v3 sky(const orc_scene* s, ray_t r) {
+    if (s->sky == 1) return V(0, 0, 0);                                 /* black :97-98 */
+    v3 unit_dir = vunit(r.d);                                           /* sky-color :91-95 */
+    double t = 0.5 * (1.0 + unit_dir.y);
+    return vadd(vscale(V(1, 1, 1), 1 - t), vscale(V(0.5, 0.7, 1.0), t));
+}
+
+typedef struct { uint64_t segments; int max_depth; } orc_counters;
+
+/* main.scm:100-121 — recursive colour */
+static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters* cnt) {
+    hitrec rec;
+    const orc_obj* w = &s->obj[s->world];
+    cnt->segments++;
+    if (depth > cnt->max_depth) cnt->max_depth = depth;
+    if (!hit_list(s, w->first, w->count, r, ORC_TMIN, ORC_TMAX, &rec)) return sky(s, r);
+    const orc_mat* m = &s->mat[rec.mat];
+    switch (m->type) {
+    case MAT_LAMBERTIAN: {                                              /* material.scm:24-39 */
+        onb_t uvw = make_onb_from_w(rec.n);
+        v3 target = onb_local(uvw, random_cosine_direction(g));
+        ray_t scattered = {rec.p, vunit(target), 0.0};
+        v3 att = tex_value(s, m->tex, 0, 0, rec.p);
+        double pdf = vdot(uvw.w, scattered.d) / ORC_PI;
+        if (depth < ORC_MAX_DEPTH) {
+            double cosine = vdot(rec.n, vunit(scattered.d));
+            if (cosine < 0) cosine = 0;
+            double spdf = cosine / ORC_PI;
+            v3 L = color(s, scattered, depth + 1, g, cnt);
+            /* emitted (0,0,0) + ((att*spdf) (*) L) * (1/pdf) */
+            return vadd(V(0, 0, 0), vscale(vmul(vscale(att, spdf), L), 1 / pdf));
+        }
+        return V(0, 0, 0);
+    }
+    case MAT_METAL: {                                                   /* material.scm:45-57 (R2) */
+        v3 reflected = reflect(vunit(r.d), rec.n);
+        v3 dir = vadd(reflected, vscale(random_in_unit_sphere(g), m->fuzz));
+        int valid = vdot(dir, rec.n) > 0;
+        v3 att = tex_value(s, m->tex, 0, 0, rec.p);
+        if (depth < ORC_MAX_DEPTH && valid) {
+            ray_t scattered = {rec.p, dir, 0.0};
+            return vmul(att, color(s, scattered, depth + 1, g, cnt));
+        }
+        return V(0, 0, 0);
+    }
+    case MAT_DIELECTRIC: {                                              /* material.scm:76-101 (R2) */
+        double ref_idx = m->ref_idx;
+        v3 reflected = reflect(r.d, rec.n);
+        double dd = vdot(r.d, rec.n);
+        v3 outward = (dd > 0) ? vscale(rec.n, -1) : rec.n;
+        double ni = (dd > 0) ? ref_idx : 1 / ref_idx;
+        double cosine = (dd > 0) ? (dd * ref_idx) / vlength(r.d) : (-dd) / vlength(r.d);
+        v3 refracted;
+        int ok = refract(r.d, outward, ni, &refracted);
+        double reflect_prob = ok ? schlick(cosine, ref_idx) : 1;
+        ray_t scattered;
+        scattered.o = rec.p; scattered.time = 0.0;
+        scattered.d = (orc_random_real(g) < reflect_prob) ? reflected : refracted;
+        if (depth < ORC_MAX_DEPTH) return vmul(V(1, 1, 1), color(s, scattered, depth + 1, g, cnt));
+        return V(0, 0, 0);
+    }
+    case MAT_DIFFUSE_LIGHT:                                             /* material.scm:103-111 */
+        if (vdot(rec.n, r.d) < 0.0) return tex_value(s, m->tex, rec.u, rec.v, rec.p);
+        return V(0, 0, 0);
+    }
+    return V(0, 0, 0);
+}
+
+/* camera.scm:80-92 — get-ray */
+static ray_t get_ray(const double* cam, double s_, double t_, orc_rng* g) {
+    v3 llc = V(cam[0], cam[1], cam[2]), hor = V(cam[3], cam[4], cam[5]), ver = V(cam[6], cam[7], cam[8]);
+    v3 origin = V(cam[9], cam[10], cam[11]);
+    v3 u = V(cam[15], cam[16], cam[17]), v = V(cam[18], cam[19], cam[20]);
+    double lens = cam[21], t0 = cam[22], t1 = cam[23];
+    v3 rd = vscale(random_in_unit_disk(g), lens);
+    v3 offset = vadd(vscale(u, rd.x), vscale(v, rd.y));
+    double time = t0 + orc_random_real(g) * (t1 - t0);
+    ray_t r;
+    r.o = vadd(origin, offset);
+    r.d = vsub(vsub(vadd(vadd(llc, vscale(hor, s_)), vscale(ver, t_)), origin), offset);
+    r.time = time;
+    return r;
+}
+
+/* One camera sample of pixel (x, y), sample index smp (0-based pass index):
+ * the body of trace-all (main.scm:476-479). */
+static v3 sample_pixel(const orc_scene* s, int nx, int ny, int x, int y, uint64_t seed, uint32_t smp,
+                       orc_counters* cnt) {
+    orc_rng g = {(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)(y * nx + x), smp, 0};
+    double u = (x + orc_random_real(&g)) / nx;
+    double v = (y + orc_random_real(&g)) / ny;
+    ray_t r = get_ray(s->cam, u, v, &g);
+    return color(s, r, 0, &g, cnt);
+}
+
+void orc_sample(const orc_scene* s, int nx, int ny, int x, int y, uint64_t seed, uint32_t smp,
+                double out[3]) {
+    orc_counters cnt = {0, 0};
+    v3 c = sample_pixel(s, nx, ny, x, y, seed, smp, &cnt);
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+}
+
+/* Render pixels [pix_begin, pix_end) of an nx*ny image, passes spp_begin ..
+ * spp_begin+spp_count-1, adding each sample colour to accum in sample order
+ * (the *raw-data* running sum, main.scm:480,488).  nthreads > 1 uses OpenMP
+ * over pixels (pixels are independent; per-pixel order is preserved).
+ * Returns the number of ray segments (closest-hit queries). */
+uint64_t orc_render(const orc_scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
+                    double* accum, long pix_begin, long pix_end, int nthreads) {
+    uint64_t total = 0;
+    if (pix_end < 0 || pix_end > (long)nx * ny) pix_end = (long)nx * ny;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+#endif
+    for (long j = pix_begin; j < pix_end; ++j) {
+        int x = (int)(j % nx), y = (int)(j / nx);
+        orc_counters cnt = {0, 0};
+        double r = accum[3 * j], gg = accum[3 * j + 1], b = accum[3 * j + 2];
+        for (int k = 0; k < spp_count; ++k) {
+            v3 c = sample_pixel(s, nx, ny, x, y, seed, (uint32_t)(spp_begin + k), &cnt);
+            r = r + c.x; gg = gg + c.y; b = b + c.z;
+        }
+        accum[3 * j] = r; accum[3 * j + 1] = gg; accum[3 * j + 2] = b;
+        total += cnt.segments;
+    }
+    (void)nthreads;
+    return total;
+}
+
+/* main.scm:481-491 — correct-gamma of sum/count, then floor(255.99*min(1,c)) */
+void orc_resolve_u8(const double* accum, long npix, int count, uint8_t* out) {
+    for (long i = 0; i < 3 * npix; ++i) {
+        double c = sqrt(accum[i] / count);
+        double m = (1 < c) ? 1.0 : c;
+        out[i] = (uint8_t)floor(255.99 * m);
+    }
+}

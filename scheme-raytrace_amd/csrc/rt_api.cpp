@@ -1,0 +1,775 @@
+// rt_api.cpp — C ABI (include/rt.h) of librtamd: scene builder, flattening
+// of the reference's object tree into grouped leaves, device upload and the
+// wavefront driver loop (raygen → [extend → shade/compact]* → accumulate).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "rt_device.h"
+
+namespace rtamd {
+hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
+hipError_t launch_extend(const DevScene&, const PathState&, uint32_t, const HitBuf&, hipStream_t);
+hipError_t launch_shade(const DevScene&, const RenderParams&, const PathState&, const HitBuf&, uint32_t,
+                        const PathState&, uint32_t*, hipStream_t);
+hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
+hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
+}  // namespace rtamd
+
+using namespace rtamd;
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string& msg) { g_err = msg; return 1; }
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)
+
+// ------------------------------------------------------------- objects
+enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH };
+
+struct Obj {
+    ObjType type;
+    int mat = -1, child = -1, axis = 0;
+    std::vector<int> kids;
+    double c0[3] = {0, 0, 0}, c1[3] = {0, 0, 0};
+    double r = 0, t0 = 0, t1 = 0;
+    double a0 = 0, a1 = 0, b0 = 0, b1 = 0, k = 0;
+    double sin_t = 0, cos_t = 1;
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf accum_tmp, img_tmp;
+};
+
+struct Scene {
+    int ctx = -1;
+    std::vector<DevTexture> texs;
+    std::vector<DevMaterial> mats;
+    std::vector<Obj> objs;
+    double cam[RT_CAMERA_DOUBLES] = {0};
+    bool have_cam = false;
+    int sky = RT_SKY_GRADIENT;
+    std::vector<double> ranvec;
+    std::vector<int32_t> perm;
+    bool have_perlin = false;
+    bool committed = false;
+
+    // flattened + uploaded
+    DevScene dev{};
+    DevBuf d_sph, d_msph, d_rect, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm;
+    // render buffers
+    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist;
+    uint32_t* h_counts = nullptr;     // pinned
+    int pix_nx = -1, pix_ny = -1, pix_shard = -1, pix_nshard = -1;
+    uint32_t pix_n = 0;
+    bool profiling = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    rt_stats stats{};
+
+    ~Scene() {
+        if (h_counts) (void)hipHostFree(h_counts);
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    }
+};
+
+std::mutex g_mu;
+std::map<int, std::unique_ptr<Context>> g_ctx;
+std::map<int, std::unique_ptr<Scene>> g_scene;
+int g_next_ctx = 1, g_next_scene = 1;
+
+Context* get_ctx(int h) {
+    auto it = g_ctx.find(h);
+    return it == g_ctx.end() ? nullptr : it->second.get();
+}
+Scene* get_scene(int h) {
+    auto it = g_scene.find(h);
+    return it == g_scene.end() ? nullptr : it->second.get();
+}
+
+#define SCENE_OR_FAIL(s, h)                                                     \
+    std::lock_guard<std::mutex> lk_(g_mu);                                      \
+    Scene* s = get_scene(h);                                                    \
+    if (!s) return fail("invalid scene handle " + std::to_string(h));            \
+    if (s->committed) return fail("scene " + std::to_string(h) + " already committed");
+
+int check_tex(Scene* s, int t) {
+    if (t < 0 || t >= (int)s->texs.size()) return fail("invalid texture id " + std::to_string(t));
+    return 0;
+}
+int check_mat(Scene* s, int m) {
+    if (m < 0 || m >= (int)s->mats.size()) return fail("invalid material id " + std::to_string(m));
+    return 0;
+}
+int check_obj(Scene* s, int o) {
+    if (o < 0 || o >= (int)s->objs.size()) return fail("invalid object id " + std::to_string(o));
+    return 0;
+}
+
+// --------------------------------------------------------- flattening
+struct LeafTmp {
+    int type;          // LeafType
+    int chain;         // -1 = world
+    int flip;
+    int obj;           // source object
+};
+
+struct Flattener {
+    Scene* s;
+    std::vector<std::vector<ChainOpRec>> chains;   // unique chains
+    std::vector<LeafTmp> leaves;                   // DFS order
+    std::vector<ChainOpRec> cur;
+    int depth_guard = 0;
+
+    int chain_id() {
+        if (cur.empty()) return -1;
+        for (size_t i = 0; i < chains.size(); ++i) {
+            if (chains[i].size() == cur.size() &&
+                std::memcmp(chains[i].data(), cur.data(), cur.size() * sizeof(ChainOpRec)) == 0)
+                return (int)i;
+        }
+        chains.push_back(cur);
+        return (int)chains.size() - 1;
+    }
+    int walk(int id, int flip) {
+        if (++depth_guard > 10000) return fail("object graph too deep (cycle?)");
+        const Obj& o = s->objs[id];
+        int rc = 0;
+        switch (o.type) {
+        case O_SPHERE: leaves.push_back({LEAF_SPHERE, chain_id(), flip, id}); break;
+        case O_MSPHERE: leaves.push_back({LEAF_MSPHERE, chain_id(), flip, id}); break;
+        case O_RECT: leaves.push_back({LEAF_RECT_XY + o.axis, chain_id(), flip, id}); break;
+        case O_FLIP: rc = walk(o.child, flip ^ 1); break;
+        case O_BOX:
+        case O_LIST:
+        case O_BVH:
+            for (int k : o.kids) { if ((rc = walk(k, flip))) break; }
+            break;
+        case O_TRANSLATE:
+        case O_ROTATE_Y: {
+            if ((int)cur.size() >= kMaxChain) return fail("instance nesting deeper than 4 transforms");
+            ChainOpRec op{};
+            if (o.type == O_TRANSLATE) { op.op = OP_TRANSLATE; op.x = o.c0[0]; op.y = o.c0[1]; op.z = o.c0[2]; }
+            else { op.op = OP_ROTATE_Y; op.x = o.sin_t; op.y = o.cos_t; op.z = 0; }
+            cur.push_back(op);
+            rc = walk(o.child, flip);
+            cur.pop_back();
+            break;
+        }
+        }
+        --depth_guard;
+        return rc;
+    }
+};
+
+template <class T>
+int upload(DevBuf& b, const std::vector<T>& v, const T** out) {
+    size_t n = std::max<size_t>(1, v.size()) * sizeof(T);
+    HIPCHK(b.ensure(n));
+    if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = b.as<const T>();
+    return 0;
+}
+
+int commit_scene(Scene* s, int world) {
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    HIPCHK(hipSetDevice(c->device));
+    if (!s->have_cam) return fail("rt_scene_commit: no camera set (rt_set_camera)");
+    for (const auto& t : s->texs)
+        if ((t.type == TEX_NOISE || t.type == TEX_MARBLE) && !s->have_perlin)
+            return fail("rt_scene_commit: noise/marble texture needs rt_set_perlin_tables");
+    Flattener f{s};
+    if (int rc = f.walk(world, 0)) return rc;
+
+    // group leaves by (chain, type) in first-appearance order of chains
+    std::vector<int> chain_order;   // -1 first
+    chain_order.push_back(-1);
+    for (size_t i = 0; i < f.chains.size(); ++i) chain_order.push_back((int)i);
+    std::vector<SphereRec> sph;
+    std::vector<MSphereRec> msph;
+    std::vector<RectRec> rect;
+    std::vector<Group> groups;
+    struct LeafOut { LeafInfo li; };
+    std::vector<LeafInfo> lsph, lmsph, lrect[3];
+    for (int ch : chain_order) {
+        for (int type = LEAF_SPHERE; type <= LEAF_RECT_YZ; ++type) {
+            Group g{type, ch, 0, 0};
+            size_t before = (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size() : rect.size();
+            g.begin = (int)before;
+            for (const LeafTmp& L : f.leaves) {
+                if (L.chain != ch || L.type != type) continue;
+                const Obj& o = s->objs[L.obj];
+                LeafInfo li{};
+                li.type = type; li.group = (int)groups.size(); li.mat = o.mat; li.flip = L.flip;
+                if (type == LEAF_SPHERE) {
+                    li.local = (int)sph.size();
+                    sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
+                    li.inv_r = 1.0 / o.r; li.radius = o.r;
+                    lsph.push_back(li);
+                } else if (type == LEAF_MSPHERE) {
+                    li.local = (int)msph.size();
+                    MSphereRec m{};
+                    m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
+                    m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
+                    m.t0 = o.t0; m.den = o.t1 - o.t0;
+                    msph.push_back(m);
+                    li.inv_r = 1.0 / o.r; li.radius = o.r;
+                    lmsph.push_back(li);
+                } else {
+                    li.local = (int)rect.size();
+                    RectRec r{};
+                    r.a0 = o.a0; r.a1 = o.a1; r.b0 = o.b0; r.b1 = o.b1; r.k = o.k;
+                    rect.push_back(r);
+                    lrect[type - LEAF_RECT_XY].push_back(li);
+                }
+            }
+            size_t after = (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size() : rect.size();
+            g.end = (int)after;
+            if (after > before) groups.push_back(g);
+        }
+    }
+    // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
+    std::vector<LeafInfo> leaves;
+    int32_t base[5];
+    base[LEAF_SPHERE] = 0;
+    for (auto& li : lsph) leaves.push_back(li);
+    base[LEAF_MSPHERE] = (int32_t)leaves.size();
+    for (auto& li : lmsph) leaves.push_back(li);
+    // rect arrays are shared between the three axis types; leaf id = rect_base + local
+    int32_t rect_base = (int32_t)leaves.size();
+    std::vector<LeafInfo> rl(rect.size());
+    for (int a = 0; a < 3; ++a) for (auto& li : lrect[a]) rl[li.local] = li;
+    for (auto& li : rl) leaves.push_back(li);
+    base[LEAF_RECT_XY] = base[LEAF_RECT_XZ] = base[LEAF_RECT_YZ] = rect_base;
+
+    std::vector<Chain> chains;
+    for (auto& cv : f.chains) {
+        Chain c{};
+        c.n = (int)cv.size();
+        for (size_t k = 0; k < cv.size(); ++k) c.ops[k] = cv[k];
+        chains.push_back(c);
+    }
+    DevScene& d = s->dev;
+    std::memset(&d, 0, sizeof d);
+    if (int rc = upload(s->d_sph, sph, &d.sph)) return rc;
+    if (int rc = upload(s->d_msph, msph, &d.msph)) return rc;
+    if (int rc = upload(s->d_rect, rect, &d.rect)) return rc;
+    if (int rc = upload(s->d_groups, groups, &d.groups)) return rc;
+    if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
+    if (int rc = upload(s->d_leaves, leaves, &d.leaves)) return rc;
+    if (int rc = upload(s->d_mats, s->mats, &d.mats)) return rc;
+    if (int rc = upload(s->d_texs, s->texs, &d.texs)) return rc;
+    d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();
+    d.n_groups = (int)groups.size(); d.n_chains = (int)chains.size(); d.n_leaves = (int)leaves.size();
+    d.n_mats = (int)s->mats.size(); d.n_texs = (int)s->texs.size();
+    for (int k = 0; k < 5; ++k) d.leaf_base[k] = base[k];
+    d.has_perlin = s->have_perlin ? 1 : 0;
+    if (s->have_perlin) {
+        if (int rc = upload(s->d_ranvec, s->ranvec, &d.ranvec)) return rc;
+        if (int rc = upload(s->d_perm, s->perm, &d.perm)) return rc;
+    }
+    d.sky = s->sky;
+    const double* cm = s->cam;
+    for (int k = 0; k < 3; ++k) {
+        d.cam.llc[k] = cm[k]; d.cam.hor[k] = cm[3 + k]; d.cam.ver[k] = cm[6 + k];
+        d.cam.origin[k] = cm[9 + k]; d.cam.w[k] = cm[12 + k]; d.cam.u[k] = cm[15 + k]; d.cam.v[k] = cm[18 + k];
+    }
+    d.cam.lens = cm[21]; d.cam.t0 = cm[22]; d.cam.t1 = cm[23];
+    for (const Obj& o : s->objs)
+        if (o.mat >= (int)s->mats.size()) return fail("object refers to an unknown material");
+    s->committed = true;
+    return 0;
+}
+
+// -------------------------------------------------------------- render
+// Interleaved 16x16 tiles (row-major tile order); tile t -> shard t % nshard.
+std::vector<uint32_t> make_pixlist(int nx, int ny, int shard, int nshard) {
+    const int T = 16;
+    const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
+    std::vector<uint32_t> out;
+    out.reserve((size_t)nx * ny / nshard + T * T);
+    for (int t = 0; t < tx * ty; ++t) {
+        if (t % nshard != shard) continue;
+        const int bx = (t % tx) * T, by = (t / tx) * T;
+        for (int yy = by; yy < std::min(by + T, ny); ++yy)
+            for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
+    }
+    return out;
+}
+
+size_t max_paths() {
+    const char* e = std::getenv("RTAMD_MAX_PATHS");
+    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)8 << 20;
+    return v < 1024 ? 1024 : v;
+}
+
+constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 5 * sizeof(uint32_t);
+
+PathState carve_state(void* base, size_t cap) {
+    PathState st;
+    double* dp = static_cast<double*>(base);
+    st.ox = dp; st.oy = dp + cap; st.oz = dp + 2 * cap; st.dx = dp + 3 * cap; st.dy = dp + 4 * cap;
+    st.dz = dp + 5 * cap; st.tm = dp + 6 * cap; st.tr = dp + 7 * cap; st.tg = dp + 8 * cap; st.tb = dp + 9 * cap;
+    uint32_t* up = reinterpret_cast<uint32_t*>(dp + 10 * cap);
+    st.pix = up; st.smp = up + cap; st.wid = up + 2 * cap; st.rng = up + 3 * cap; st.depth = up + 4 * cap;
+    return st;
+}
+
+int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, int shard,
+                int nshard, double* accum, hipStream_t stream) {
+    if (!s->committed) return fail("scene not committed (rt_scene_commit)");
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if (spp_begin < 0 || spp_count < 0) return fail("spp_begin/spp_count must be >= 0");
+    if (nshard <= 0 || shard < 0 || shard >= nshard) return fail("invalid shard index/count");
+    if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    HIPCHK(hipSetDevice(c->device));
+    if (!stream) stream = c->stream;
+    auto t_start = std::chrono::steady_clock::now();
+    std::memset(&s->stats, 0, sizeof s->stats);
+    if (spp_count == 0) return 0;
+
+    if (s->pix_nx != nx || s->pix_ny != ny || s->pix_shard != shard || s->pix_nshard != nshard) {
+        std::vector<uint32_t> pl = make_pixlist(nx, ny, shard, nshard);
+        HIPCHK(s->pixlist.ensure(std::max<size_t>(1, pl.size()) * sizeof(uint32_t)));
+        if (!pl.empty()) HIPCHK(hipMemcpy(s->pixlist.p, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        s->pix_nx = nx; s->pix_ny = ny; s->pix_shard = shard; s->pix_nshard = nshard;
+        s->pix_n = (uint32_t)pl.size();
+    }
+    const uint32_t npix = s->pix_n;
+    if (npix == 0) return 0;
+    const size_t cap_paths = max_paths();
+    uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
+    if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
+    const size_t cap = (size_t)npix * chunk;
+    if (cap >= (1ull << 32)) return fail("path pool too large");
+    HIPCHK(s->st_a.ensure(cap * kStateBytesPerPath));
+    HIPCHK(s->st_b.ensure(cap * kStateBytesPerPath));
+    HIPCHK(s->hit_t.ensure(cap * sizeof(double)));
+    HIPCHK(s->hit_leaf.ensure(cap * sizeof(int32_t)));
+    HIPCHK(s->sb.ensure(cap * 3 * sizeof(double)));
+    HIPCHK(s->counts.ensure((kMaxDepth + 4) * sizeof(uint32_t)));
+    if (!s->h_counts) HIPCHK(hipHostMalloc((void**)&s->h_counts, (kMaxDepth + 4) * sizeof(uint32_t)));
+    if (s->profiling && !s->ev[0])
+        for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+
+    PathState A = carve_state(s->st_a.p, cap), Bst = carve_state(s->st_b.p, cap);
+    HitBuf hit{s->hit_t.as<double>(), s->hit_leaf.as<int32_t>()};
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+
+    for (int done = 0; done < spp_count; done += (int)chunk) {
+        const uint32_t S = (uint32_t)std::min<int>((int)chunk, spp_count - done);
+        RenderParams rp{};
+        rp.nx = (uint32_t)nx; rp.ny = (uint32_t)ny; rp.npix = npix;
+        rp.spp0 = (uint32_t)(spp_begin + done); rp.k0 = k0; rp.k1 = k1;
+        rp.pixlist = s->pixlist.as<const uint32_t>();
+        rp.sb = s->sb.as<double>();
+        rp.B = npix * S;
+        HIPCHK(hipMemsetAsync(s->counts.p, 0, (kMaxDepth + 4) * sizeof(uint32_t), stream));
+        HIPCHK(launch_raygen(s->dev, rp, A, stream));
+        PathState* cur = &A;
+        PathState* nxt = &Bst;
+        uint32_t n = rp.B;
+        s->stats.paths += rp.B;
+        for (int depth = 0; n > 0; ++depth) {
+            if (depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
+            uint32_t* dcount = s->counts.as<uint32_t>() + depth;
+            if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
+            HIPCHK(launch_extend(s->dev, *cur, n, hit, stream));
+            if (s->profiling) HIPCHK(hipEventRecord(s->ev[1], stream));
+            HIPCHK(launch_shade(s->dev, rp, *cur, hit, n, *nxt, dcount, stream));
+            if (s->profiling) HIPCHK(hipEventRecord(s->ev[2], stream));
+            HIPCHK(hipMemcpyAsync(s->h_counts + depth, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            if (s->profiling) {
+                float a = 0, b = 0;
+                HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
+                HIPCHK(hipEventElapsedTime(&b, s->ev[1], s->ev[2]));
+                s->stats.ms_extend += a; s->stats.ms_shade += b;
+            }
+            s->stats.segments += n;
+            s->stats.extend_launches += 1;
+            if ((uint32_t)depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)depth;
+            n = s->h_counts[depth];
+            std::swap(cur, nxt);
+        }
+        HIPCHK(launch_accumulate(rp, S, accum, stream));
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    s->stats.extend_rays = s->stats.segments;
+    s->stats.ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return 0;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(int* out) {
+    if (!out) return fail("null out pointer");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    *out = n;
+    return 0;
+}
+
+int rt_context_create(int device, int* out_ctx) {
+    if (!out_ctx) return fail("null out pointer");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail("device " + std::to_string(device) + " out of range (" + std::to_string(n) + " devices)");
+    HIPCHK(hipSetDevice(device));
+    auto c = std::make_unique<Context>();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    std::lock_guard<std::mutex> lk(g_mu);
+    int h = g_next_ctx++;
+    g_ctx[h] = std::move(c);
+    *out_ctx = h;
+    return 0;
+}
+
+int rt_context_destroy(int ctx) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    for (auto it = g_scene.begin(); it != g_scene.end();) {
+        if (it->second->ctx == ctx) it = g_scene.erase(it); else ++it;
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    g_ctx.erase(ctx);
+    return 0;
+}
+
+int rt_scene_begin(int ctx, int* out_scene) {
+    if (!out_scene) return fail("null out pointer");
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!get_ctx(ctx)) return fail("invalid context handle");
+    auto s = std::make_unique<Scene>();
+    s->ctx = ctx;
+    int h = g_next_scene++;
+    g_scene[h] = std::move(s);
+    *out_scene = h;
+    return 0;
+}
+
+int rt_scene_destroy(int scene) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_scene.erase(scene)) return fail("invalid scene handle");
+    return 0;
+}
+
+#define OUT_OR_FAIL(p) if (!(p)) return fail("null out pointer")
+
+int rt_add_texture_constant(int scene, const double rgb[3], int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    DevTexture t{};
+    t.type = TEX_CONSTANT; t.r = rgb[0]; t.g = rgb[1]; t.bl = rgb[2];
+    s->texs.push_back(t);
+    *out = (int)s->texs.size() - 1;
+    return 0;
+}
+int rt_add_texture_checker(int scene, int even, int odd, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_tex(s, even) || check_tex(s, odd)) return 1;
+    DevTexture t{};
+    t.type = TEX_CHECKER; t.a = even; t.b = odd;
+    s->texs.push_back(t);
+    *out = (int)s->texs.size() - 1;
+    return 0;
+}
+static int add_scaled_tex(int scene, int type, double sc, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    DevTexture t{};
+    t.type = type; t.scale = sc;
+    s->texs.push_back(t);
+    *out = (int)s->texs.size() - 1;
+    return 0;
+}
+int rt_add_texture_noise(int scene, double sc, int* out) { return add_scaled_tex(scene, TEX_NOISE, sc, out); }
+int rt_add_texture_marble(int scene, double sc, int* out) { return add_scaled_tex(scene, TEX_MARBLE, sc, out); }
+
+static int add_mat(int scene, int type, int tex, double fuzz, double ref, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (type != MAT_DIELECTRIC && check_tex(s, tex)) return 1;
+    DevMaterial m{};
+    m.type = type; m.tex = tex; m.fuzz = fuzz; m.ref_idx = ref;
+    s->mats.push_back(m);
+    *out = (int)s->mats.size() - 1;
+    return 0;
+}
+int rt_add_material_lambertian(int scene, int tex, int* out) { return add_mat(scene, MAT_LAMBERTIAN, tex, 0, 0, out); }
+int rt_add_material_metal(int scene, int tex, double fuzz, int* out) { return add_mat(scene, MAT_METAL, tex, fuzz, 0, out); }
+int rt_add_material_dielectric(int scene, double ref, int* out) { return add_mat(scene, MAT_DIELECTRIC, -1, 0, ref, out); }
+int rt_add_material_diffuse_light(int scene, int tex, int* out) { return add_mat(scene, MAT_DIFFUSE_LIGHT, tex, 0, 0, out); }
+
+static int push_obj(Scene* s, Obj&& o, int* out) {
+    s->objs.push_back(std::move(o));
+    *out = (int)s->objs.size() - 1;
+    return 0;
+}
+
+int rt_add_sphere(int scene, const double c[3], double r, int mat, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_mat(s, mat)) return 1;
+    Obj o; o.type = O_SPHERE; o.mat = mat; o.r = r;
+    for (int k = 0; k < 3; ++k) o.c0[k] = c[k];
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_moving_sphere(int scene, const double c0[3], const double c1[3], double t0, double t1, double r,
+                         int mat, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_mat(s, mat)) return 1;
+    Obj o; o.type = O_MSPHERE; o.mat = mat; o.r = r; o.t0 = t0; o.t1 = t1;
+    for (int k = 0; k < 3; ++k) { o.c0[k] = c0[k]; o.c1[k] = c1[k]; }
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1, double k, int mat, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (axis < 0 || axis > 2) return fail("rect axis must be RT_RECT_XY/XZ/YZ");
+    if (check_mat(s, mat)) return 1;
+    Obj o; o.type = O_RECT; o.axis = axis; o.mat = mat;
+    o.a0 = a0; o.a1 = a1; o.b0 = b0; o.b1 = b1; o.k = k;
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_flip_normals(int scene, int child, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_obj(s, child)) return 1;
+    Obj o; o.type = O_FLIP; o.child = child; o.mat = s->objs[child].mat;
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_box(int scene, const double p0[3], const double p1[3], int mat, int* out) {
+    // geometry.scm:444-463 — six rects, back faces flipped, in this order
+    int r[6], tmp;
+    if (rt_add_rect(scene, RT_RECT_XY, p0[0], p1[0], p0[1], p1[1], p1[2], mat, &r[0])) return 1;
+    if (rt_add_rect(scene, RT_RECT_XY, p0[0], p1[0], p0[1], p1[1], p0[2], mat, &tmp)) return 1;
+    if (rt_add_flip_normals(scene, tmp, &r[1])) return 1;
+    if (rt_add_rect(scene, RT_RECT_XZ, p0[0], p1[0], p0[2], p1[2], p1[1], mat, &r[2])) return 1;
+    if (rt_add_rect(scene, RT_RECT_XZ, p0[0], p1[0], p0[2], p1[2], p0[1], mat, &tmp)) return 1;
+    if (rt_add_flip_normals(scene, tmp, &r[3])) return 1;
+    if (rt_add_rect(scene, RT_RECT_YZ, p0[1], p1[1], p0[2], p1[2], p1[0], mat, &r[4])) return 1;
+    if (rt_add_rect(scene, RT_RECT_YZ, p0[1], p1[1], p0[2], p1[2], p0[0], mat, &tmp)) return 1;
+    if (rt_add_flip_normals(scene, tmp, &r[5])) return 1;
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    Obj o; o.type = O_BOX; o.mat = mat; o.kids.assign(r, r + 6);
+    for (int k = 0; k < 3; ++k) { o.c0[k] = p0[k]; o.c1[k] = p1[k]; }
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_translate(int scene, int child, const double off[3], int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_obj(s, child)) return 1;
+    Obj o; o.type = O_TRANSLATE; o.child = child; o.mat = s->objs[child].mat;
+    for (int k = 0; k < 3; ++k) o.c0[k] = off[k];
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_rotate_y(int scene, int child, double angle, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_obj(s, child)) return 1;
+    Obj o; o.type = O_ROTATE_Y; o.child = child; o.mat = s->objs[child].mat;
+    const double radians = (kPi / 180.0) * angle;     // geometry.scm:484
+    o.sin_t = std::sin(radians); o.cos_t = std::cos(radians);
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_list(int scene, const int* objs, int n, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (n < 0 || (n > 0 && !objs)) return fail("invalid object list");
+    Obj o; o.type = O_LIST;
+    for (int i = 0; i < n; ++i) { if (check_obj(s, objs[i])) return 1; o.kids.push_back(objs[i]); }
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_bvh(int scene, const int* objs, int n, double t0, double t1, int sah, int* out) {
+    (void)t0; (void)t1; (void)sah;
+    if (rt_add_list(scene, objs, n, out)) return 1;
+    std::lock_guard<std::mutex> lk(g_mu);
+    get_scene(scene)->objs[*out].type = O_BVH;
+    return 0;
+}
+
+int rt_make_camera(const double from[3], const double at[3], const double vup[3], double vfov, double aspect,
+                   double aperture, double focus, double t0, double t1, double out[RT_CAMERA_DOUBLES]) {
+    if (!out) return fail("null out pointer");
+    // camera.scm:63-78 in the reference's evaluation order
+    auto sub = [](const double* a, const double* b, double* r) { for (int k = 0; k < 3; ++k) r[k] = a[k] - b[k]; };
+    auto unit = [](const double* a, double* r) {
+        double d = 0.0; d += a[0] * a[0]; d += a[1] * a[1]; d += a[2] * a[2];
+        const double k = 1.0 / std::sqrt(d);
+        for (int i = 0; i < 3; ++i) r[i] = a[i] * k;
+    };
+    auto cross = [](const double* a, const double* b, double* r) {
+        r[0] = a[1] * b[2] - b[1] * a[2]; r[1] = a[2] * b[0] - b[2] * a[0]; r[2] = a[0] * b[1] - b[0] * a[1];
+    };
+    const double theta = vfov * (kPi / 180.0);
+    const double hh = std::tan(theta / 2);
+    const double hw = aspect * hh;
+    double w[3], u[3], v[3], tmp[3];
+    sub(from, at, tmp); unit(tmp, w);
+    cross(vup, w, tmp); unit(tmp, u);
+    cross(w, u, v);
+    for (int k = 0; k < 3; ++k) {
+        double llc = from[k] - u[k] * (hw * focus);
+        llc = llc - v[k] * (hh * focus);
+        llc = llc - w[k] * focus;
+        out[k] = llc;
+        out[3 + k] = u[k] * (2 * hw * focus);
+        out[6 + k] = v[k] * (2 * hh * focus);
+        out[9 + k] = from[k];
+        out[12 + k] = w[k]; out[15 + k] = u[k]; out[18 + k] = v[k];
+    }
+    out[21] = aperture / 2; out[22] = t0; out[23] = t1;
+    return 0;
+}
+
+int rt_set_camera(int scene, const double cam[RT_CAMERA_DOUBLES]) {
+    SCENE_OR_FAIL(s, scene);
+    if (!cam) return fail("null camera");
+    std::memcpy(s->cam, cam, sizeof s->cam);
+    s->have_cam = true;
+    return 0;
+}
+int rt_set_sky(int scene, int sky) {
+    SCENE_OR_FAIL(s, scene);
+    if (sky != RT_SKY_GRADIENT && sky != RT_SKY_BLACK) return fail("sky must be RT_SKY_GRADIENT or RT_SKY_BLACK");
+    s->sky = sky;
+    return 0;
+}
+int rt_set_perlin_tables(int scene, const double ranvec[768], const int32_t px[256], const int32_t py[256],
+                         const int32_t pz[256]) {
+    SCENE_OR_FAIL(s, scene);
+    if (!ranvec || !px || !py || !pz) return fail("null Perlin table");
+    s->ranvec.assign(ranvec, ranvec + 768);
+    s->perm.resize(768);
+    for (int i = 0; i < 256; ++i) {
+        if (px[i] < 0 || px[i] > 255 || py[i] < 0 || py[i] > 255 || pz[i] < 0 || pz[i] > 255)
+            return fail("Perlin permutation entries must be in 0..255");
+        s->perm[i] = px[i]; s->perm[256 + i] = py[i]; s->perm[512 + i] = pz[i];
+    }
+    s->have_perlin = true;
+    return 0;
+}
+int rt_scene_commit(int scene, int world) {
+    SCENE_OR_FAIL(s, scene);
+    if (check_obj(s, world)) return 1;
+    return commit_scene(s, world);
+}
+
+int rt_set_profiling(int scene, int enabled) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    s->profiling = enabled != 0;
+    return 0;
+}
+
+int rt_get_stats(int scene, rt_stats* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!out) return fail("null out pointer");
+    *out = s->stats;
+    return 0;
+}
+
+int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, int shard,
+                     int nshard, double* accum, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!accum) return fail("null accum");
+    return render_impl(s, nx, ny, spp_begin, spp_count, seed, shard, nshard, accum, (hipStream_t)stream);
+}
+
+int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, double* accum_host) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!accum_host) return fail("null accum");
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t bytes = (size_t)nx * ny * 3 * sizeof(double);
+    HIPCHK(c->accum_tmp.ensure(bytes));
+    HIPCHK(hipMemcpyAsync(c->accum_tmp.p, accum_host, bytes, hipMemcpyHostToDevice, c->stream));
+    if (int rc = render_impl(s, nx, ny, spp_begin, spp_count, seed, 0, 1, c->accum_tmp.as<double>(), c->stream))
+        return rc;
+    HIPCHK(hipMemcpyAsync(accum_host, c->accum_tmp.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int rt_resolve_u8(const double* accum, int nx, int ny, int count, uint8_t* out) {
+    if (!accum || !out) return fail("null buffer");
+    if (count <= 0) return fail("sample_count must be positive");
+    const size_t n = (size_t)nx * ny * 3;
+    for (size_t i = 0; i < n; ++i) {
+        const double c = std::sqrt(accum[i] / count);
+        const double m = (1.0 < c) ? 1.0 : c;
+        out[i] = (uint8_t)std::floor(255.99 * m);
+    }
+    return 0;
+}
+
+int rt_resolve_u8_device(int ctx, const double* accum, int nx, int ny, int count, uint8_t* out, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    if (!accum || !out) return fail("null buffer");
+    if (count <= 0) return fail("sample_count must be positive");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(launch_resolve_u8(accum, (uint32_t)((size_t)nx * ny * 3), count, out, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+}  // extern "C"

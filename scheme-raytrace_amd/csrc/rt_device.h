@@ -1,0 +1,102 @@
+// rt_device.h — device-side scene and wavefront-state layout (HBM).
+//
+// The reference evaluates closest hit by calling one closure per object of a
+// linked list (geometry.scm:33-50) and nested closures for flip / box /
+// translate / rotate-y (geometry.scm:433-543).  Here the host flattens that
+// object tree into *leaf primitives*, each tagged with an instance chain
+// (translate / rotate-y ops, outermost first) and a flip parity, and groups
+// leaves of one type under one chain so the extend kernel runs one uniform,
+// type-specialised loop per group with the primitive parameters read through
+// the scalar unit (every lane of a wave tests the same primitive).
+#pragma once
+#include <stdint.h>
+
+namespace rtamd {
+
+constexpr int kMaxDepth = 100;                 // main.scm:26
+constexpr double kTmin = 0.001;                // main.scm:104
+constexpr double kTmax = 999999999999.0;       // constant.scm:6
+constexpr double kPi = 3.141592653589793;      // math.const pi
+constexpr int kMaxChain = 4;                   // instance ops per leaf chain
+
+enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
+enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
+enum LeafType : int32_t { LEAF_SPHERE = 0, LEAF_MSPHERE = 1, LEAF_RECT_XY = 2, LEAF_RECT_XZ = 3,
+                          LEAF_RECT_YZ = 4 };
+enum ChainOp : int32_t { OP_TRANSLATE = 0, OP_ROTATE_Y = 1 };
+
+struct DevTexture {            // texture.scm:12-34
+    int32_t type, a, b, pad;   // checker: a = even, b = odd
+    double r, g, bl, scale;
+};
+struct DevMaterial {           // material.scm:24-111
+    int32_t type, tex;
+    double fuzz, ref_idx;
+};
+
+// Extend-side records: only what the closest-hit test reads, 16-B aligned so
+// the scalar unit fetches each with one s_load_dwordx8 / x16.
+struct alignas(32) SphereRec { double cx, cy, cz, rr; };             // rr = r*r
+struct alignas(64) MSphereRec {                                        // center(t) = c0 + dc*((t-t0)/den)
+    double c0x, c0y, c0z, rr, dcx, dcy, dcz, t0;
+    double den, pad0, pad1, pad2;
+};
+struct alignas(64) RectRec { double a0, a1, b0, b1, k, pad0, pad1, pad2; };
+
+// Shade-side per-leaf record (indexed by leaf id).
+struct LeafInfo {
+    int32_t type, group, local, mat;   // local = index in the type's array
+    int32_t flip, pad0, pad1, pad2;
+    double inv_r;                      // sphere: (/ 1 radius) as a double
+    double radius;
+};
+
+struct ChainOpRec { int32_t op, pad; double x, y, z; };   // translate: (x,y,z); rotate: x=sin, y=cos
+struct Chain { int32_t n, pad; ChainOpRec ops[kMaxChain]; };
+
+// One group = leaves [begin, end) of one type under one chain (-1 = world).
+struct Group { int32_t type, chain, begin, end; };   // begin/end index the type array
+                                                      // leaf id = leaf_base[type] + local
+
+struct DevCamera {            // camera.scm:33-78 (the 10 slots)
+    double llc[3], hor[3], ver[3], origin[3], w[3], u[3], v[3];
+    double lens, t0, t1;
+};
+
+struct DevScene {
+    const SphereRec* sph;  int32_t n_sph;
+    const MSphereRec* msph; int32_t n_msph;
+    const RectRec* rect;   int32_t n_rect;
+    const Group* groups;   int32_t n_groups;
+    const Chain* chains;   int32_t n_chains;
+    const LeafInfo* leaves; int32_t n_leaves;
+    int32_t leaf_base[5];                      // first leaf id of each LeafType
+    const DevMaterial* mats; int32_t n_mats;
+    const DevTexture* texs;  int32_t n_texs;
+    const double* ranvec;                      // 256*3 (Perlin)
+    const int32_t* perm;                       // 3*256 (x, y, z)
+    int32_t has_perlin;
+    int32_t sky;                               // 0 gradient, 1 black
+    DevCamera cam;
+};
+
+// Wavefront path state, SoA, one slot per live path (ping-pong buffers).
+struct PathState {
+    double *ox, *oy, *oz, *dx, *dy, *dz, *tm;   // ray
+    double *tr, *tg, *tb;                        // throughput
+    uint32_t *pix, *smp, *wid, *rng, *depth;     // pixel, absolute sample, work id, draw counter, depth
+};
+struct HitBuf { double* t; int32_t* leaf; };
+
+// Per-render-chunk parameters shared by the kernels.
+struct RenderParams {
+    uint32_t nx, ny;
+    uint32_t npix;            // pixels of this shard
+    uint32_t spp0;            // absolute sample index of the chunk's first sample
+    uint32_t k0, k1;          // RNG key (seed)
+    const uint32_t* pixlist;  // shard pixel q -> image pixel j
+    double* sb;               // sample colours [3][B] SoA, B = npix * chunk_spp
+    uint32_t B;
+};
+
+}  // namespace rtamd

@@ -1,0 +1,172 @@
+"""Device side of the drop-in: contexts, scene upload and rendering through
+librtamd's C ABI.  There is no CPU fallback anywhere in this module."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, dvec, out_int
+from .scene import emit
+
+_default_ctx = {}
+
+
+class Context:
+    """A librtamd context on one HIP device (rt_context_create)."""
+
+    def __init__(self, device=0):
+        h = out_int()
+        call("rt_context_create", int(device), ctypes.byref(h))
+        self.handle = h.value
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            call("rt_context_destroy", self.handle)
+            self.handle = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_context(device=0):
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]
+
+
+def device_count():
+    n = out_int()
+    call("rt_device_count", ctypes.byref(n))
+    return n.value
+
+
+class GpuBuilder:
+    """Replays a scene descriptor graph into rt_add_* calls (scene.emit)."""
+
+    def __init__(self, ctx):
+        h = out_int()
+        call("rt_scene_begin", ctx.handle, ctypes.byref(h))
+        self.scene = h.value
+
+    def _out(self, name, *args):
+        o = out_int()
+        call(name, self.scene, *args, ctypes.byref(o))
+        return o.value
+
+    def texture_constant(self, rgb):
+        return self._out("rt_add_texture_constant", dvec(rgb))
+
+    def texture_checker(self, even, odd):
+        return self._out("rt_add_texture_checker", even, odd)
+
+    def texture_noise(self, sc):
+        return self._out("rt_add_texture_noise", sc)
+
+    def texture_marble(self, sc):
+        return self._out("rt_add_texture_marble", sc)
+
+    def material_lambertian(self, tex):
+        return self._out("rt_add_material_lambertian", tex)
+
+    def material_metal(self, tex, fuzz):
+        return self._out("rt_add_material_metal", tex, fuzz)
+
+    def material_dielectric(self, ref_idx):
+        return self._out("rt_add_material_dielectric", ref_idx)
+
+    def material_diffuse_light(self, tex):
+        return self._out("rt_add_material_diffuse_light", tex)
+
+    def sphere(self, c, r, mat):
+        return self._out("rt_add_sphere", dvec(c), r, mat)
+
+    def moving_sphere(self, c0, c1, t0, t1, r, mat):
+        return self._out("rt_add_moving_sphere", dvec(c0), dvec(c1), t0, t1, r, mat)
+
+    def rect(self, axis, a0, a1, b0, b1, k, mat):
+        return self._out("rt_add_rect", axis, a0, a1, b0, b1, k, mat)
+
+    def flip_normals(self, obj):
+        return self._out("rt_add_flip_normals", obj)
+
+    def box(self, p0, p1, mat):
+        return self._out("rt_add_box", dvec(p0), dvec(p1), mat)
+
+    def translate(self, obj, off):
+        return self._out("rt_add_translate", obj, dvec(off))
+
+    def rotate_y(self, obj, angle):
+        return self._out("rt_add_rotate_y", obj, angle)
+
+    def list(self, objs):
+        arr = (ctypes.c_int * max(1, len(objs)))(*objs)
+        return self._out("rt_add_list", arr, len(objs))
+
+    def bvh(self, objs, t0, t1, sah):
+        arr = (ctypes.c_int * max(1, len(objs)))(*objs)
+        return self._out("rt_add_bvh", arr, len(objs), t0, t1, sah)
+
+    def set_camera(self, slots):
+        call("rt_set_camera", self.scene, dvec(slots))
+
+    def set_sky(self, code):
+        call("rt_set_sky", self.scene, code)
+
+    def set_perlin(self, ranvec, px, py, pz):
+        i32 = ctypes.c_int32 * 256
+        call("rt_set_perlin_tables", self.scene, dvec(ranvec), i32(*px), i32(*py), i32(*pz))
+
+    def commit(self, world):
+        call("rt_scene_commit", self.scene, world)
+        return self.scene
+
+
+def upload(scene, ctx=None):
+    """Commit a scene (rtamd.scene.Scene) on ctx; cached per context."""
+    ctx = ctx or default_context()
+    h = scene._handles.get(ctx.handle)
+    if h is None:
+        h = emit(scene, GpuBuilder(ctx))
+        scene._handles[ctx.handle] = h
+    return h
+
+
+def stats(scene_handle):
+    s = _lib.RtStats()
+    call("rt_get_stats", scene_handle, ctypes.byref(s))
+    return s
+
+
+def render_host(scene, nx, ny, spp_begin, spp_count, seed, accum, ctx=None):
+    """rt_render: accum is a host float64 array of nx*ny*3 (updated in place)."""
+    h = upload(scene, ctx)
+    a = np.ascontiguousarray(accum, dtype=np.float64)
+    if a.size != nx * ny * 3:
+        raise ValueError("accum must have nx*ny*3 elements")
+    call("rt_render", h, nx, ny, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)),
+         a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if a is not accum:
+        accum[...] = a.reshape(accum.shape)
+    return h
+
+
+def render_device(scene, nx, ny, spp_begin, spp_count, seed, accum_ptr, shard=0, nshard=1, stream=None,
+                  ctx=None):
+    """rt_render_device: accum_ptr is a device pointer (int) to nx*ny*3 doubles."""
+    h = upload(scene, ctx)
+    call("rt_render_device", h, nx, ny, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)), shard,
+         nshard, ctypes.c_void_p(accum_ptr), ctypes.c_void_p(stream or 0))
+    return h
+
+
+def resolve_u8(accum, nx, ny, sample_count):
+    """rt_resolve_u8 (main.scm:481-491) on the host."""
+    a = np.ascontiguousarray(accum, dtype=np.float64).ravel()
+    out = np.zeros(nx * ny * 3, dtype=np.uint8)
+    call("rt_resolve_u8", a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), nx, ny, int(sample_count),
+         out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return out
