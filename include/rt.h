@@ -131,8 +131,10 @@ typedef struct rt_stats {
     double   ms_shade;    /* summed device time of the shade kernel */
     uint64_t extend_launches;
     uint64_t extend_rays; /* = segments */
-    uint32_t max_depth_seen;
+    uint32_t max_depth_seen;  /* deepest wavefront iteration (the tail runs in k_finish) */
     uint32_t reserved;
+    double   ms_finish;       /* summed device time of the tail kernel */
+    uint64_t finish_paths;    /* paths handed to the tail kernel */
 } rt_stats;
 int rt_get_stats(int scene, rt_stats* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */

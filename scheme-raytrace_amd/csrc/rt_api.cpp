@@ -3,6 +3,7 @@
 // wavefront driver loop (raygen → [extend → shade/compact]* → accumulate).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -19,9 +20,12 @@
 
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
-hipError_t launch_extend(const DevScene&, const PathState&, uint32_t, const HitBuf&, hipStream_t);
-hipError_t launch_shade(const DevScene&, const RenderParams&, const PathState&, const HitBuf&, uint32_t,
-                        const PathState&, uint32_t*, hipStream_t);
+hipError_t launch_extend(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
+                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, hipStream_t);
+hipError_t launch_shade(int, const DevScene&, const RenderParams&, const PathState&, const HitBuf&,
+                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, hipStream_t);
+hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
+                         unsigned long long*, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 }  // namespace rtamd
@@ -88,9 +92,9 @@ struct Scene {
 
     // flattened + uploaded
     DevScene dev{};
-    DevBuf d_sph, d_msph, d_rect, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm;
+    DevBuf d_sph, d_msph, d_rect, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh, d_bvh2, d_bleaf;
     // render buffers
-    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist;
+    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
     uint32_t* h_counts = nullptr;     // pinned
     int pix_nx = -1, pix_ny = -1, pix_shard = -1, pix_nshard = -1;
     uint32_t pix_n = 0;
@@ -193,6 +197,109 @@ struct Flattener {
     }
 };
 
+// ------------------------------------------------------------------ BVH
+// Binned-SAH BVH over the world-level spheres / moving spheres, traversed
+// wave-uniformly by k_extend (rt_kernels.hip bvh_closest).  Boxes are padded
+// outward (relative 1e-8) so culling is conservative and the closest hit is
+// exactly the flat list's (geometry.scm:33-50), ties aside.  Moving spheres
+// are bounded over every time a ray can carry: camera rays in [time0, time1],
+// scattered rays at 0 (Q4, Q13).
+struct PrimRef { double lo[3], hi[3], c[3]; int leaf; bool moving; };
+
+struct BvhBuild {
+    std::vector<PrimRef>& refs;
+    std::vector<BvhNode> nodes;
+    static constexpr int kLeafMax = 4;
+    static constexpr int kBins = 16;
+
+    static double area(const double* lo, const double* hi) {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (dx < 0 || dy < 0 || dz < 0) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+    static void grow(double* lo, double* hi, const double* plo, const double* phi) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], plo[k]); hi[k] = std::max(hi[k], phi[k]); }
+    }
+    int make_leaf(int node, int b, int e, const double* lo, const double* hi) {
+        BvhNode& N = nodes[node];
+        for (int k = 0; k < 3; ++k) { N.lo[k] = lo[k]; N.hi[k] = hi[k]; }
+        N.a = b; N.b = e; N.c = -2; N.d = 0;        // ranges fixed up after the build
+        return node;
+    }
+    int build(int b, int e, int depth) {
+        const int node = (int)nodes.size();
+        nodes.push_back(BvhNode{});
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
+        for (int i = b; i < e; ++i) { grow(lo, hi, refs[i].lo, refs[i].hi); grow(clo, chi, refs[i].c, refs[i].c); }
+        const int n = e - b;
+        if (n <= kLeafMax || depth >= kLaneStack - 2) return make_leaf(node, b, e, lo, hi);
+        int axis = 0;
+        for (int k = 1; k < 3; ++k) if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        const double ext = chi[axis] - clo[axis];
+        int mid = -1;
+        if (ext > 0) {
+            int cnt[kBins] = {0};
+            double blo[kBins][3], bhi[kBins][3];
+            for (int k = 0; k < kBins; ++k) for (int j = 0; j < 3; ++j) { blo[k][j] = 1e300; bhi[k][j] = -1e300; }
+            auto bin_of = [&](const PrimRef& r) {
+                int k = (int)((r.c[axis] - clo[axis]) / ext * kBins);
+                return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+            };
+            for (int i = b; i < e; ++i) { const int k = bin_of(refs[i]); cnt[k]++; grow(blo[k], bhi[k], refs[i].lo, refs[i].hi); }
+            double best = 1e300;
+            int best_k = -1;
+            for (int k = 1; k < kBins; ++k) {
+                double llo[3] = {1e300, 1e300, 1e300}, lhi[3] = {-1e300, -1e300, -1e300};
+                double rlo[3] = {1e300, 1e300, 1e300}, rhi[3] = {-1e300, -1e300, -1e300};
+                int nl = 0, nr = 0;
+                for (int j = 0; j < k; ++j) if (cnt[j]) { grow(llo, lhi, blo[j], bhi[j]); nl += cnt[j]; }
+                for (int j = k; j < kBins; ++j) if (cnt[j]) { grow(rlo, rhi, blo[j], bhi[j]); nr += cnt[j]; }
+                if (!nl || !nr) continue;
+                const double c = area(llo, lhi) * nl + area(rlo, rhi) * nr;
+                if (c < best) { best = c; best_k = k; }
+            }
+            const double parent = area(lo, hi);
+            const bool worth = best_k > 0 && (parent <= 0 || 0.5 + best / parent < (double)n);
+            if (!worth && n <= 2 * kLeafMax) return make_leaf(node, b, e, lo, hi);
+            if (best_k > 0) {
+                auto it = std::partition(refs.begin() + b, refs.begin() + e,
+                                         [&](const PrimRef& r) { return bin_of(r) < best_k; });
+                mid = (int)(it - refs.begin());
+            }
+        }
+        if (mid <= b || mid >= e) {                  // degenerate: median split on the axis
+            mid = b + n / 2;
+            std::nth_element(refs.begin() + b, refs.begin() + mid, refs.begin() + e,
+                             [&](const PrimRef& x, const PrimRef& y) { return x.c[axis] < y.c[axis]; });
+        }
+        const int l = build(b, mid, depth + 1);
+        const int r = build(mid, e, depth + 1);
+        BvhNode& N = nodes[node];
+        for (int k = 0; k < 3; ++k) { N.lo[k] = lo[k]; N.hi[k] = hi[k]; }
+        N.a = l; N.b = r; N.c = -1; N.d = axis;
+        return node;
+    }
+};
+
+void pad_box(double* lo, double* hi) {
+    double m = 1.0;
+    for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
+    const double pad = 1e-8 * m;
+    for (int k = 0; k < 3; ++k) { lo[k] -= pad; hi[k] += pad; }
+}
+
+int traversal_mode() {
+    const char* e = std::getenv("RTAMD_TRAVERSAL");
+    if (e && std::strcmp(e, "wave") == 0) return TRAV_WAVE;
+    return TRAV_LANE;
+}
+
+size_t bvh_min_prims() {
+    const char* e = std::getenv("RTAMD_BVH_MIN");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : 16;
+}
+
 template <class T>
 int upload(DevBuf& b, const std::vector<T>& v, const T** out) {
     size_t n = std::max<size_t>(1, v.size()) * sizeof(T);
@@ -221,10 +328,103 @@ int commit_scene(Scene* s, int world) {
     std::vector<MSphereRec> msph;
     std::vector<RectRec> rect;
     std::vector<Group> groups;
-    struct LeafOut { LeafInfo li; };
     std::vector<LeafInfo> lsph, lmsph, lrect[3];
+
+    // BVH over the world-level (chain -1) spheres and moving spheres
+    std::vector<PrimRef> refs;
+    for (size_t i = 0; i < f.leaves.size(); ++i) {
+        const LeafTmp& L = f.leaves[i];
+        if (L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE)) continue;
+        const Obj& o = s->objs[L.obj];
+        PrimRef r{};
+        r.leaf = (int)i;
+        r.moving = L.type == LEAF_MSPHERE;
+        const double rad = std::fabs(o.r);
+        if (!r.moving) {
+            for (int k = 0; k < 3; ++k) { r.lo[k] = o.c0[k] - rad; r.hi[k] = o.c0[k] + rad; }
+        } else {
+            const double den = o.t1 - o.t0;
+            const double ct0 = s->cam[22], ct1 = s->cam[23];
+            const double tlo = std::min(std::min(ct0, ct1), 0.0), thi = std::max(std::max(ct0, ct1), 0.0);
+            if (!(den != 0.0) || !std::isfinite(den)) {
+                for (int k = 0; k < 3; ++k) { r.lo[k] = -1e300; r.hi[k] = 1e300; }
+            } else {
+                const double f0 = (tlo - o.t0) / den, f1 = (thi - o.t0) / den;
+                for (int k = 0; k < 3; ++k) {
+                    const double dc = o.c1[k] - o.c0[k];
+                    const double a = o.c0[k] + dc * f0, b = o.c0[k] + dc * f1;
+                    r.lo[k] = std::min(a, b) - rad; r.hi[k] = std::max(a, b) + rad;
+                }
+            }
+        }
+        pad_box(r.lo, r.hi);
+        for (int k = 0; k < 3; ++k) r.c[k] = 0.5 * (r.lo[k] + r.hi[k]);
+        refs.push_back(r);
+    }
+    const bool use_bvh = !refs.empty() && refs.size() >= bvh_min_prims();
+    std::vector<BvhNode> bvh_nodes;
+    std::vector<BvhNode2> bvh2;
+    std::vector<BvhLeaf> bleaf;
+    int32_t bvh2_root = 0;
+    if (use_bvh) {
+        BvhBuild bb{refs, {}};
+        bb.build(0, (int)refs.size(), 0);
+        // leaf ranges: refs order -> sphere / moving-sphere array indices
+        std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0);
+        for (size_t i = 0; i < refs.size(); ++i) {
+            ns[i + 1] = ns[i] + (refs[i].moving ? 0 : 1);
+            nm[i + 1] = nm[i] + (refs[i].moving ? 1 : 0);
+        }
+        for (BvhNode& N : bb.nodes) {
+            if (N.c != -2) continue;
+            const int b = N.a, e = N.b;
+            N.a = ns[b]; N.b = ns[e] - ns[b]; N.c = nm[b]; N.d = nm[e] - nm[b];
+        }
+        bvh_nodes = std::move(bb.nodes);
+        // per-lane layout: child boxes in the parent
+        std::vector<int> inner_idx(bvh_nodes.size(), -1), leaf_idx(bvh_nodes.size(), -1);
+        for (size_t i = 0; i < bvh_nodes.size(); ++i) {
+            if (bvh_nodes[i].c < 0) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); }
+            else { leaf_idx[i] = (int)bleaf.size(); bleaf.push_back({bvh_nodes[i].a, bvh_nodes[i].b, bvh_nodes[i].c, bvh_nodes[i].d}); }
+        }
+        auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
+        for (size_t i = 0; i < bvh_nodes.size(); ++i) {
+            if (inner_idx[i] < 0) continue;
+            BvhNode2& M = bvh2[inner_idx[i]];
+            const BvhNode& L = bvh_nodes[bvh_nodes[i].a];
+            const BvhNode& R = bvh_nodes[bvh_nodes[i].b];
+            for (int k = 0; k < 3; ++k) {
+                M.lbox[k] = L.lo[k]; M.lbox[3 + k] = L.hi[k]; M.rbox[k] = R.lo[k]; M.rbox[3 + k] = R.hi[k];
+            }
+            M.l = ref_of(bvh_nodes[i].a); M.r = ref_of(bvh_nodes[i].b);
+        }
+        bvh2_root = ref_of(0);
+        const int gid = (int)groups.size();
+        groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
+        for (const PrimRef& r : refs) {
+            const LeafTmp& L = f.leaves[r.leaf];
+            const Obj& o = s->objs[L.obj];
+            LeafInfo li{};
+            li.type = L.type; li.group = gid; li.mat = o.mat; li.flip = L.flip;
+            li.inv_r = 1.0 / o.r; li.radius = o.r;
+            if (!r.moving) {
+                li.local = (int)sph.size();
+                sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
+                lsph.push_back(li);
+            } else {
+                li.local = (int)msph.size();
+                MSphereRec m{};
+                m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
+                m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
+                m.t0 = o.t0; m.den = o.t1 - o.t0;
+                msph.push_back(m);
+                lmsph.push_back(li);
+            }
+        }
+    }
     for (int ch : chain_order) {
         for (int type = LEAF_SPHERE; type <= LEAF_RECT_YZ; ++type) {
+            if (use_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE)) continue;
             Group g{type, ch, 0, 0};
             size_t before = (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size() : rect.size();
             g.begin = (int)before;
@@ -287,6 +487,13 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_msph, msph, &d.msph)) return rc;
     if (int rc = upload(s->d_rect, rect, &d.rect)) return rc;
     if (int rc = upload(s->d_groups, groups, &d.groups)) return rc;
+    if (int rc = upload(s->d_bvh, bvh_nodes, &d.bvh)) return rc;
+    d.n_bvh = (int)bvh_nodes.size();
+    if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
+    if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
+    d.n_bvh2 = (int)bvh2.size();
+    d.bvh2_root = bvh2_root;
+    d.traversal = traversal_mode();
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
     if (int rc = upload(s->d_leaves, leaves, &d.leaves)) return rc;
     if (int rc = upload(s->d_mats, s->mats, &d.mats)) return rc;
@@ -301,6 +508,8 @@ int commit_scene(Scene* s, int world) {
         if (int rc = upload(s->d_perm, s->perm, &d.perm)) return rc;
     }
     d.sky = s->sky;
+    d.mat_mask = 0;
+    for (const auto& m : s->mats) d.mat_mask |= 1 << m.type;
     const double* cm = s->cam;
     for (int k = 0; k < 3; ++k) {
         d.cam.llc[k] = cm[k]; d.cam.hor[k] = cm[3 + k]; d.cam.ver[k] = cm[6 + k];
@@ -331,8 +540,13 @@ std::vector<uint32_t> make_pixlist(int nx, int ny, int shard, int nshard) {
 
 size_t max_paths() {
     const char* e = std::getenv("RTAMD_MAX_PATHS");
-    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)8 << 20;
+    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)32 << 20;
     return v < 1024 ? 1024 : v;
+}
+
+uint32_t tail_threshold() {
+    const char* e = std::getenv("RTAMD_TAIL_PATHS");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 32768u;
 }
 
 constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 5 * sizeof(uint32_t);
@@ -375,20 +589,34 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     const size_t cap = (size_t)npix * chunk;
-    if (cap >= (1ull << 32)) return fail("path pool too large");
-    HIPCHK(s->st_a.ensure(cap * kStateBytesPerPath));
-    HIPCHK(s->st_b.ensure(cap * kStateBytesPerPath));
-    HIPCHK(s->hit_t.ensure(cap * sizeof(double)));
-    HIPCHK(s->hit_leaf.ensure(cap * sizeof(int32_t)));
+    // sharded compaction (rt_device.h kShards): shard capacity bounds what the
+    // blocks of one shard can append in one wavefront step (extend: one item
+    // per thread; the four shade kernels: grid-stride over at most 4096 blocks)
+    const size_t gmax = std::min<size_t>(4096, (cap + 255) / 256 + kShards);
+    const size_t shard_cap = (cap + kShards - 1) / kShards + 4 * 32 * gmax + 256;
+    const size_t scap = shard_cap * kShards;
+    if (scap >= (1ull << 32)) return fail("path pool too large");
+    HIPCHK(s->st_a.ensure(scap * kStateBytesPerPath));
+    HIPCHK(s->st_b.ensure(scap * kStateBytesPerPath));
+    HIPCHK(s->hit_t.ensure(scap * sizeof(double)));
+    HIPCHK(s->hit_leaf.ensure(scap * sizeof(int32_t)));
     HIPCHK(s->sb.ensure(cap * 3 * sizeof(double)));
-    HIPCHK(s->counts.ensure((kMaxDepth + 4) * sizeof(uint32_t)));
-    if (!s->h_counts) HIPCHK(hipHostMalloc((void**)&s->h_counts, (kMaxDepth + 4) * sizeof(uint32_t)));
+    constexpr int kCountsPerIter = 5 * kShards;   // 4 material queues + survivors, 8 shards each
+    constexpr int kIters = kMaxDepth + 4;
+    HIPCHK(s->counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
+    HIPCHK(s->queues.ensure(scap * 4 * sizeof(uint32_t)));
+    HIPCHK(s->seg_tail.ensure(sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(s->seg_tail.p, 0, sizeof(unsigned long long), stream));
+    if (!s->h_counts) HIPCHK(hipHostMalloc((void**)&s->h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
     if (s->profiling && !s->ev[0])
         for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
 
-    PathState A = carve_state(s->st_a.p, cap), Bst = carve_state(s->st_b.p, cap);
+    PathState A = carve_state(s->st_a.p, scap), Bst = carve_state(s->st_b.p, scap);
     HitBuf hit{s->hit_t.as<double>(), s->hit_leaf.as<int32_t>()};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t* queues = s->queues.as<uint32_t>();
+    const uint32_t qstride = (uint32_t)scap;
+    const int mat_mask = s->dev.mat_mask;
 
     for (int done = 0; done < spp_count; done += (int)chunk) {
         const uint32_t S = (uint32_t)std::min<int>((int)chunk, spp_count - done);
@@ -398,38 +626,71 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         rp.pixlist = s->pixlist.as<const uint32_t>();
         rp.sb = s->sb.as<double>();
         rp.B = npix * S;
-        HIPCHK(hipMemsetAsync(s->counts.p, 0, (kMaxDepth + 4) * sizeof(uint32_t), stream));
+        // below the tail threshold one k_finish launch completes every
+        // remaining path (extend + shade looped per thread)
+        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / 128u);
+        HIPCHK(hipMemsetAsync(s->counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), stream));
         HIPCHK(launch_raygen(s->dev, rp, A, stream));
         PathState* cur = &A;
         PathState* nxt = &Bst;
+        QView view{nullptr, (uint32_t)scap};         // raygen output: contiguous
         uint32_t n = rp.B;
         s->stats.paths += rp.B;
         for (int depth = 0; n > 0; ++depth) {
             if (depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
-            uint32_t* dcount = s->counts.as<uint32_t>() + depth;
+            if (n <= tail) {
+                if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
+                HIPCHK(launch_finish(s->dev, rp, *cur, view, n, s->seg_tail.as<unsigned long long>(), stream));
+                if (s->profiling) {
+                    HIPCHK(hipEventRecord(s->ev[1], stream));
+                    HIPCHK(hipEventSynchronize(s->ev[1]));
+                    float a = 0;
+                    HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
+                    s->stats.ms_finish += a;
+                }
+                s->stats.finish_paths += n;
+                break;
+            }
+            uint32_t* cnt = s->counts.as<uint32_t>() + depth * kCountsPerIter;   // [class][shard], survivors at 4
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
-            HIPCHK(launch_extend(s->dev, *cur, n, hit, stream));
+            HIPCHK(launch_extend(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt, stream));
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[1], stream));
-            HIPCHK(launch_shade(s->dev, rp, *cur, hit, n, *nxt, dcount, stream));
+            uint32_t* surv = cnt + 4 * kShards;
+            for (int mt = 0; mt < 4; ++mt) {
+                if (!(mat_mask & (1 << mt))) continue;
+                const QView qv{cnt + mt * kShards, (uint32_t)shard_cap};
+                HIPCHK(launch_shade(mt, s->dev, rp, *cur, hit, queues + (size_t)mt * qstride, qv, n, *nxt, surv,
+                                    (uint32_t)shard_cap, stream));
+            }
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[2], stream));
-            HIPCHK(hipMemcpyAsync(s->h_counts + depth, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipMemcpyAsync(s->h_counts + depth * kCountsPerIter, surv, kShards * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             if (s->profiling) {
                 float a = 0, b = 0;
                 HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
                 HIPCHK(hipEventElapsedTime(&b, s->ev[1], s->ev[2]));
                 s->stats.ms_extend += a; s->stats.ms_shade += b;
+                s->stats.extend_launches += 1;
             }
+            s->stats.extend_rays += n;
             s->stats.segments += n;
-            s->stats.extend_launches += 1;
             if ((uint32_t)depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)depth;
-            n = s->h_counts[depth];
+            n = 0;
+            for (int x = 0; x < kShards; ++x) {
+                const uint32_t c_x = s->h_counts[depth * kCountsPerIter + x];
+                if (c_x > shard_cap) return fail("internal: shard overflow");
+                n += c_x;
+            }
+            view = QView{surv, (uint32_t)shard_cap};
             std::swap(cur, nxt);
         }
         HIPCHK(launch_accumulate(rp, S, accum, stream));
     }
     HIPCHK(hipStreamSynchronize(stream));
-    s->stats.extend_rays = s->stats.segments;
+    unsigned long long tail_segs = 0;
+    HIPCHK(hipMemcpy(&tail_segs, s->seg_tail.p, sizeof tail_segs, hipMemcpyDeviceToHost));
+    s->stats.segments += tail_segs;
     s->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return 0;

@@ -23,6 +23,7 @@ enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_M
 enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum LeafType : int32_t { LEAF_SPHERE = 0, LEAF_MSPHERE = 1, LEAF_RECT_XY = 2, LEAF_RECT_XZ = 3,
                           LEAF_RECT_YZ = 4 };
+constexpr int32_t GROUP_BVH = 5;               // group type: BVH over world-level spheres
 enum ChainOp : int32_t { OP_TRANSLATE = 0, OP_ROTATE_Y = 1 };
 
 struct DevTexture {            // texture.scm:12-34
@@ -42,6 +43,22 @@ struct alignas(64) MSphereRec {                                        // center
     double den, pad0, pad1, pad2;
 };
 struct alignas(64) RectRec { double a0, a1, b0, b1, k, pad0, pad1, pad2; };
+
+// BVH node over the world-level spheres and moving spheres (64 B = one
+// s_load_dwordx16).  Boxes are padded outward so culling is conservative: the
+// primitive tests are the exact f64 ones, the BVH only skips primitives that
+// cannot report a hit.  inner: c = -1, a/b = children, d = split axis;
+// leaf: spheres [a, a+b), moving spheres [c, c+d).
+struct alignas(64) BvhNode { double lo[3], hi[3]; int32_t a, b, c, d; };
+constexpr int kBvhStack = 64;                  // per-wave traversal stack (LDS)
+
+// Per-lane traversal layout (Aila & Laine style BVH2): both child boxes live
+// in the parent so one visit tests two boxes.  Child refs: >= 0 inner node,
+// < 0 leaf ~index into BvhLeaf.
+struct alignas(16) BvhNode2 { double lbox[6]; double rbox[6]; int32_t l, r, pad0, pad1; };
+struct BvhLeaf { int32_t sb, sn, mb, mn; };       // spheres [sb,sb+sn), moving [mb,mb+mn)
+constexpr int kLaneStack = 32;                 // per-lane traversal stack (LDS, stride = block size)
+enum Traversal : int32_t { TRAV_WAVE = 0, TRAV_LANE = 1 };
 
 // Shade-side per-leaf record (indexed by leaf id).
 struct LeafInfo {
@@ -68,6 +85,10 @@ struct DevScene {
     const MSphereRec* msph; int32_t n_msph;
     const RectRec* rect;   int32_t n_rect;
     const Group* groups;   int32_t n_groups;
+    const BvhNode* bvh;    int32_t n_bvh;
+    const BvhNode2* bvh2;  int32_t n_bvh2;
+    const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)
+    int32_t traversal;                             // Traversal
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
     int32_t leaf_base[5];                      // first leaf id of each LeafType
@@ -77,6 +98,7 @@ struct DevScene {
     const int32_t* perm;                       // 3*256 (x, y, z)
     int32_t has_perlin;
     int32_t sky;                               // 0 gradient, 1 black
+    int32_t mat_mask;                          // bit t set <=> some material of type t exists
     DevCamera cam;
 };
 
@@ -87,6 +109,14 @@ struct PathState {
     uint32_t *pix, *smp, *wid, *rng, *depth;     // pixel, absolute sample, work id, draw counter, depth
 };
 struct HitBuf { double* t; int32_t* leaf; };
+
+// Sharded queues.  Stream compaction appends through one atomic per block
+// and class on a counter chosen by blockIdx % kShards (8 XCDs), so no single
+// counter word serialises the chip; shard x of a queue holds counts[x] entries
+// at [x*cap, x*cap + counts[x]).  Consumers see a virtual index space
+// 0..sum(counts)-1 (QView; counts == nullptr means "contiguous").
+constexpr int kShards = 8;
+struct QView { const uint32_t* counts; uint32_t cap; };
 
 // Per-render-chunk parameters shared by the kernels.
 struct RenderParams {

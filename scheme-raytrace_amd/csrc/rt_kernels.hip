@@ -5,11 +5,15 @@
 //
 //   k_raygen    trace-all jitter + cam:get-ray      main.scm:476-478, camera.scm:80-92
 //   k_extend    closest hit over the flattened       geometry.scm:14-56,146-215,376-543
-//               object tree (one segment per path)
-//   k_shade     hit record + material scatter +      material.scm:15-111, texture.scm,
-//               sky / emission; survivors compacted  perlin.scm, main.scm:91-121
-//               with a wave64 ballot + mbcnt prefix
-//               and one atomic per wave
+//               object tree (one segment per path);  main.scm:91-95,120
+//               misses finish with the sky, hits are
+//               appended to per-material queues
+//   k_shade<M>  hit record + material M's scatter /  material.scm:15-111, texture.scm,
+//               emission; survivors compacted with   perlin.scm, main.scm:100-121
+//               a wave64 ballot + mbcnt prefix and
+//               one atomic per wave
+//   k_finish    the depth tail: extend+shade looped  (same code, one thread per path)
+//               per thread for the last few paths
 //   k_accumulate per-pixel running sum in sample     main.scm:480,488
 //               order (deterministic, no atomics)
 //   k_resolve_u8 correct-gamma + quantise            main.scm:481-491
@@ -142,21 +146,152 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
     st.pix[w] = j; st.smp[w] = smp; st.wid[w] = w; st.rng[w] = g.ctr; st.depth[w] = 0u;
 }
 
-// =====================================================================
-// k_extend — closest hit (hit-obj-list semantics: shrinking t-max,
-// strict (tmin, closest) for spheres, non-strict for rects)
-// =====================================================================
-__global__ __launch_bounds__(256) void k_extend(const DevScene sc, const PathState st, uint32_t n,
-                                                HitBuf hit) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    const v3 o0 = mk(st.ox[i], st.oy[i], st.oz[i]);
-    const v3 d0 = mk(st.dx[i], st.dy[i], st.dz[i]);
-    const double time = st.tm[i];
-    double closest = kTmax;
+// ---------------------------------------------------------- closest hit
+// hit-obj-list semantics (geometry.scm:33-50): shrinking t-max, strict
+// (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
+// walks the same group / primitive sequence, so the primitive records are
+// fetched once per wave through the scalar unit.
+// sphere test (geometry.scm:146-171); updates closest/best on a hit
+__device__ __forceinline__ void sphere_test(const v3 o, const v3 d, const double a, const v3 c, const double rr,
+                                            const int32_t id, double& closest, int32_t& best) {
+    const v3 oc = o - c;
+    const double b = dot(oc, d);
+    const double cc = dot(oc, oc) - rr;
+    const double disc = b * b - a * cc;
+    if (disc > 0.0) {
+        const double sq = sqrt(disc);
+        double t = (-b - sq) / a;
+        if (!(kTmin < t && t < closest)) t = (-b + sq) / a;
+        if (kTmin < t && t < closest) { closest = t; best = id; }
+    }
+}
+
+// Conservative slab test of a padded BVH box against [0, closest].
+__device__ __forceinline__ bool box_hit(const BvhNode& N, const v3 o, const v3 inv, const double closest) {
+    const double tx0 = (N.lo[0] - o.x) * inv.x, tx1 = (N.hi[0] - o.x) * inv.x;
+    const double ty0 = (N.lo[1] - o.y) * inv.y, ty1 = (N.hi[1] - o.y) * inv.y;
+    const double tz0 = (N.lo[2] - o.z) * inv.z, tz1 = (N.hi[2] - o.z) * inv.z;
+    const double tnear = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
+    const double tfar = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), closest * 1.000000001));
+    return tnear <= tfar;
+}
+
+// Wave-uniform BVH traversal: the wave enters a node if ANY of its active
+// lanes' rays hits the node's box, so node records stay on the scalar path and
+// control flow stays uniform; each lane still keeps its own closest hit, and a
+// leaf's spheres get the same exact test as the brute-force loop.
+__device__ __forceinline__ void bvh_closest(const DevScene& sc, const v3 o, const v3 d, const double time,
+                                            double& closest, int32_t& best, uint32_t* stk) {
+    const double a = dot(d, d);
+    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
+    double last_t0 = 0.0, last_den = 0.0, frac = 0.0;
+    bool have = false;
+    int sp = 0;
+    uint32_t node = 0;
+    for (;;) {
+        const BvhNode N = sc.bvh[node];
+        const bool h = box_hit(N, o, inv, closest);
+        if (__ballot(h)) {
+            if (N.c < 0) {                                    // inner: near child first
+                const double dax = (N.d == 0) ? d.x : (N.d == 1) ? d.y : d.z;
+                const int neg = __builtin_amdgcn_readfirstlane((int)(dax < 0.0));
+                const uint32_t near = neg ? (uint32_t)N.b : (uint32_t)N.a;
+                const uint32_t far = neg ? (uint32_t)N.a : (uint32_t)N.b;
+                if (sp < kBvhStack) stk[sp++] = far;
+                node = near;
+                continue;
+            }
+            for (int s = N.a; s < N.a + N.b; ++s) {
+                const SphereRec S = sc.sph[s];
+                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+            }
+            for (int s = N.c; s < N.c + N.d; ++s) {
+                const MSphereRec S = sc.msph[s];
+                if (!have || S.t0 != last_t0 || S.den != last_den) {   // uniform branch
+                    frac = (time - S.t0) / S.den;
+                    last_t0 = S.t0; last_den = S.den; have = true;
+                }
+                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+            }
+        }
+        if (sp == 0) break;
+        node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+    }
+}
+
+// Per-lane BVH traversal: every lane walks its own path through the BVH2
+// (child boxes tested at the parent, nearer child first, LDS stack with a
+// block-size stride so a wave's pushes hit 64 consecutive banks).
+__device__ __forceinline__ bool box_hit_t(const double* bx, const v3 o, const v3 inv, const double closest,
+                                          double& tnear) {
+    const double tx0 = (bx[0] - o.x) * inv.x, tx1 = (bx[3] - o.x) * inv.x;
+    const double ty0 = (bx[1] - o.y) * inv.y, ty1 = (bx[4] - o.y) * inv.y;
+    const double tz0 = (bx[2] - o.z) * inv.z, tz1 = (bx[5] - o.z) * inv.z;
+    tnear = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
+    const double tfar = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), closest * 1.000000001));
+    return tnear <= tfar;
+}
+
+__device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
+                                                 double& closest, int32_t& best, uint32_t* lstk) {
+    const double a = dot(d, d);
+    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
+    const uint32_t stride = blockDim.x;
+    int sp = 0;
+    int32_t node = sc.bvh2_root;
+    for (;;) {
+        if (node >= 0) {
+            const BvhNode2 N = sc.bvh2[node];
+            double tl, tr;
+            const bool hl = box_hit_t(N.lbox, o, inv, closest, tl);
+            const bool hr = box_hit_t(N.rbox, o, inv, closest, tr);
+            if (hl && hr) {
+                const bool lfirst = tl <= tr;
+                if (sp < kLaneStack) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                node = lfirst ? N.l : N.r;
+                continue;
+            }
+            if (hl) { node = N.l; continue; }
+            if (hr) { node = N.r; continue; }
+        } else {
+            const BvhLeaf L = sc.bleaf[~node];
+            for (int s = L.sb; s < L.sb + L.sn; ++s) {
+                const SphereRec S = sc.sph[s];
+                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+            }
+            for (int s = L.mb; s < L.mb + L.mn; ++s) {
+                const MSphereRec S = sc.msph[s];
+                const double frac = (time - S.t0) / S.den;
+                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = (int32_t)lstk[sp * stride];
+    }
+}
+
+// ---------------------------------------------------------- closest hit
+// hit-obj-list semantics (geometry.scm:33-50): shrinking t-max, strict
+// (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
+// walks the same group / primitive sequence, so the primitive records are
+// fetched once per wave through the scalar unit.
+__device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
+                                               const double time, double& closest, uint32_t* stk,
+                                               uint32_t* lstk) {
     int32_t best = -1;
+    closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
         const Group G = sc.groups[g];
+        if (G.type == GROUP_BVH) {
+            if (sc.traversal == TRAV_LANE) bvh_closest_lane(sc, o0, d0, time, closest, best, lstk);
+            else bvh_closest(sc, o0, d0, time, closest, best, stk);
+            continue;
+        }
         v3 o = o0, d = d0;
         if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
         const int32_t base = sc.leaf_base[G.type];
@@ -164,16 +299,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const PathSta
             const double a = dot(d, d);
             for (int s = G.begin; s < G.end; ++s) {
                 const SphereRec S = sc.sph[s];
-                const v3 oc = o - mk(S.cx, S.cy, S.cz);
-                const double b = dot(oc, d);
-                const double c = dot(oc, oc) - S.rr;
-                const double disc = b * b - a * c;
-                if (disc > 0.0) {
-                    const double sq = sqrt(disc);
-                    double t = (-b - sq) / a;
-                    if (!(kTmin < t && t < closest)) t = (-b + sq) / a;
-                    if (kTmin < t && t < closest) { closest = t; best = base + s; }
-                }
+                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, base + s, closest, best);
             }
         } else if (G.type == LEAF_MSPHERE) {               // geometry.scm:177-208
             const double a = dot(d, d);
@@ -186,16 +312,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const PathSta
                     last_t0 = S.t0; last_den = S.den; have = true;
                 }
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                const v3 oc = o - cen;
-                const double b = dot(oc, d);
-                const double c = dot(oc, oc) - S.rr;
-                const double disc = b * b - a * c;
-                if (disc > 0.0) {
-                    const double sq = sqrt(disc);
-                    double t = (-b - sq) / a;
-                    if (!(kTmin < t && t < closest)) t = (-b + sq) / a;
-                    if (kTmin < t && t < closest) { closest = t; best = base + s; }
-                }
+                sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
             }
         } else {                                            // geometry.scm:376-431
             // XY: k on z, (a,b) = (x,y); XZ: k on y, (x,z); YZ: k on x, (y,z)
@@ -213,8 +330,135 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const PathSta
             }
         }
     }
-    hit.t[i] = closest;
-    hit.leaf[i] = best;
+    return best;
+}
+
+// ------------------------------------------------------------ path state
+struct PathRegs {
+    v3 o, d;
+    double time;
+    v3 T;
+    uint32_t pix, smp, wid, rng, depth;
+};
+__device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathRegs& p) {
+    p.o = mk(st.ox[i], st.oy[i], st.oz[i]);
+    p.d = mk(st.dx[i], st.dy[i], st.dz[i]);
+    p.time = st.tm[i];
+    p.T = mk(st.tr[i], st.tg[i], st.tb[i]);
+    p.pix = st.pix[i]; p.smp = st.smp[i]; p.wid = st.wid[i]; p.rng = st.rng[i]; p.depth = st.depth[i];
+}
+__device__ __forceinline__ void store_path(const PathState& st, uint32_t k, const PathRegs& p) {
+    st.ox[k] = p.o.x; st.oy[k] = p.o.y; st.oz[k] = p.o.z;
+    st.dx[k] = p.d.x; st.dy[k] = p.d.y; st.dz[k] = p.d.z;
+    st.tm[k] = p.time;
+    st.tr[k] = p.T.x; st.tg[k] = p.T.y; st.tb[k] = p.T.z;
+    st.pix[k] = p.pix; st.smp[k] = p.smp; st.wid[k] = p.wid; st.rng[k] = p.rng; st.depth[k] = p.depth;
+}
+// path done: sample colour = T (*) L into the chunk's sample buffer
+__device__ __forceinline__ void write_sample(const RenderParams& rp, const PathRegs& p, const v3 L) {
+    rp.sb[p.wid] = p.T.x * L.x;
+    rp.sb[rp.B + p.wid] = p.T.y * L.y;
+    rp.sb[2u * rp.B + p.wid] = p.T.z * L.z;
+}
+__device__ __forceinline__ v3 sky_radiance(const DevScene& sc, const v3 d) {
+    if (sc.sky != 0) return mk(0.0, 0.0, 0.0);            // black main.scm:97-98
+    const v3 ud = unit(d);                                 // sky-color main.scm:91-95
+    const double s = 0.5 * (1.0 + ud.y);
+    return mk(1.0, 1.0, 1.0) * (1.0 - s) + mk(0.5, 0.7, 1.0) * s;
+}
+
+// ------------------------------------------------------ stream compaction
+// Virtual index -> physical slot of a sharded queue (QView).  The 8 shard
+// counts are wave-uniform (scalar loads); the select chain avoids dynamic
+// register indexing.
+struct QMap { uint32_t off[kShards]; uint32_t cap; bool contiguous; };
+__device__ __forceinline__ QMap qmap(const QView v) {
+    QMap m;
+    m.cap = v.cap;
+    m.contiguous = v.counts == nullptr;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int x = 0; x < kShards; ++x) { m.off[x] = acc; if (!m.contiguous) acc += v.counts[x]; }
+    return m;
+}
+__device__ __forceinline__ uint32_t qphys(const QMap& m, uint32_t k) {
+    if (m.contiguous) return k;
+    uint32_t base = 0, x = 0;
+#pragma unroll
+    for (int j = 1; j < kShards; ++j)
+        if (k >= m.off[j]) { base = m.off[j]; x = (uint32_t)j; }
+    return x * m.cap + (k - base);
+}
+
+// Block-aggregated, shard-spread stream compaction (all threads of the block
+// must call it: it holds barriers).  cls in [0, NC) selects the queue, -1 =
+// nothing to append.  Per class: wave64 ballot + mbcnt inside each wave, an
+// exclusive scan of the wave counts in LDS, ONE atomicAdd per block on the
+// counter of shard blockIdx % kShards.  Returns the item's physical slot
+// (within its class queue).
+template <int NC>
+__device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __restrict__ counts,
+                                                 const uint32_t shard_cap, uint32_t* s_cnt) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t shard = blockIdx.x & (kShards - 1);
+    uint32_t below = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const unsigned long long mask = __ballot(cls == c);
+        if (cls == c)
+            below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (lane == 0) s_cnt[c * 16 + wave] = (uint32_t)__popcll(mask);
+    }
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)NC) {
+        const int c = threadIdx.x;
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < nw; ++w) { const uint32_t v = s_cnt[c * 16 + w]; s_cnt[c * 16 + w] = tot; tot += v; }
+        s_cnt[NC * 16 + c] = tot ? atomicAdd(counts + c * kShards + shard, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t slot = 0;
+    if (cls >= 0) slot = shard * shard_cap + s_cnt[NC * 16 + cls] + s_cnt[cls * 16 + wave] + below;
+    __syncthreads();                       // s_cnt is reused by the next call
+    return slot;
+}
+
+// =====================================================================
+// k_extend — one closest-hit query per live path.  Misses are finished on
+// the spot (sky); hits are appended to the queue of their material type so
+// each shade kernel runs one material's code (wavefront material queues).
+// =====================================================================
+__global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
+                                                const PathState st, const QView in, uint32_t n, HitBuf hit,
+                                                uint32_t* __restrict__ queues, uint32_t qstride,
+                                                uint32_t shard_cap, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_stack[4 * kBvhStack];
+    __shared__ uint32_t s_lstack[256 * kLaneStack];
+    __shared__ uint32_t s_cnt[4 * 16 + 4];
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    int cls = -1;
+    uint32_t i = 0;
+    if (k < n) {
+        i = qphys(qmap(in), k);
+        const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
+        const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
+        double t;
+        const int32_t leaf = closest_hit(sc, o, d, st.tm[i], t, s_stack + (threadIdx.x >> 6) * kBvhStack,
+                                         s_lstack + threadIdx.x);
+        if (leaf < 0) {
+            const v3 L = sky_radiance(sc, d);
+            const uint32_t wid = st.wid[i];
+            rp.sb[wid] = st.tr[i] * L.x;
+            rp.sb[rp.B + wid] = st.tg[i] * L.y;
+            rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+        } else {
+            hit.t[i] = t;
+            hit.leaf[i] = leaf;
+            cls = sc.mats[sc.leaves[leaf].mat].type;
+        }
+    }
+    const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
+    if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
 }
 
 // ------------------------------------------------------------- textures
@@ -280,171 +524,185 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
 
 __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - n * (2.0 * dot(v, n)); }  // material.scm:41-43
 
-// =====================================================================
-// k_shade — hit record, scatter, emission, sky; compaction of survivors
-// =====================================================================
-__global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderParams rp,
-                                               const PathState in, const HitBuf hit, uint32_t n,
-                                               PathState out, uint32_t* __restrict__ out_count) {
-    __shared__ PerlinLds P;
-    if (sc.has_perlin) {   // stage the Perlin tables in LDS (perlin.scm:32-36 data)
-        for (int k = threadIdx.x; k < 768; k += 256) { P.ranvec[k] = sc.ranvec[k]; P.perm[k] = sc.perm[k]; }
+// ------------------------------------------------------------- shading
+// Hit record + material (material.scm:15-111).  MATF = the material type a
+// queue holds (compile-time; -1 = any, used by the tail kernel).  Returns true
+// if the path continues (p holds the scattered ray, new throughput, depth+1);
+// otherwise L is the terminal radiance (emission or 0).
+template <int MATF>
+__device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
+                                          PathRegs& p, const double t, const int32_t leaf, v3& L) {
+    L = mk(0.0, 0.0, 0.0);
+    const LeafInfo li = sc.leaves[leaf];
+    const Group G = sc.groups[li.group];
+    v3 o = p.o, d = p.d;
+    if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
+    v3 pt = o + d * t;                         // point-at-parameter on the (local) ray
+    v3 nrm;
+    if (li.type == LEAF_SPHERE) {
+        const SphereRec S = sc.sph[li.local];
+        nrm = (pt - mk(S.cx, S.cy, S.cz)) * li.inv_r;
+    } else if (li.type == LEAF_MSPHERE) {
+        const MSphereRec S = sc.msph[li.local];
+        const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * ((p.time - S.t0) / S.den);
+        nrm = (pt - cen) * li.inv_r;
+    } else if (li.type == LEAF_RECT_XY) {
+        nrm = mk(0.0, 0.0, 1.0);
+    } else if (li.type == LEAF_RECT_XZ) {
+        nrm = mk(0.0, 1.0, 0.0);
+    } else {
+        nrm = mk(1.0, 0.0, 0.0);
+    }
+    if (li.flip) nrm = nrm * -1.0;                          // flip-normals :438
+    if (G.chain >= 0) chain_hit(sc.chains[G.chain], pt, nrm);
+    const DevMaterial m = sc.mats[li.mat];
+    const int mt = (MATF >= 0) ? MATF : m.type;
+    const v3 rdir = p.d;
+    const bool can_continue = p.depth < (uint32_t)kMaxDepth;
+    if (mt == MAT_DIFFUSE_LIGHT) {                           // material.scm:103-111
+        if (dot(nrm, rdir) < 0.0) L = tex_value(sc, P, m.tex, pt);
+        return false;
+    }
+    if (!can_continue) return false;                         // depth cap (main.scm:112,119)
+    Rng g;
+    g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
+    if (mt == MAT_LAMBERTIAN) {                              // material.scm:24-39
+        // onb.scm:8-16
+        const v3 axis2 = unit(nrm);
+        const v3 a = (fabs(axis2.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+        const v3 axis1 = unit(cross(axis2, a));
+        const v3 axis0 = cross(axis2, axis1);
+        // util.scm:37-44 (x2 quirk on x and y)
+        const double r1 = g.next();
+        const double r2 = g.next();
+        const double z = sqrt(1.0 - r2);
+        const double phi = 2.0 * kPi * r1;
+        double sphi, cphi;
+        sincos(phi, &sphi, &cphi);
+        const double x = cphi * 2.0 * sqrt(r2);
+        const double y = sphi * 2.0 * sqrt(r2);
+        const v3 target = (axis0 * x + axis1 * y) + axis2 * z;   // onb `local`
+        const v3 sd = unit(target);
+        const double pdf = dot(axis2, sd) / kPi;
+        double cosine = dot(nrm, unit(sd));
+        if (cosine < 0.0) cosine = 0.0;
+        const double spdf = cosine / kPi;                    // scattering-pdf
+        const double ipdf = 1.0 / pdf;
+        const v3 att = tex_value(sc, P, m.tex, pt);
+        // forward form of  e + ((att*spdf) (*) L_next) * (1/pdf)  (main.scm:113-118)
+        p.T = mk((p.T.x * (att.x * spdf)) * ipdf, (p.T.y * (att.y * spdf)) * ipdf,
+                 (p.T.z * (att.z * spdf)) * ipdf);
+        p.d = sd;
+    } else if (mt == MAT_METAL) {                            // material.scm:45-57 (R2)
+        const v3 reflected = reflect(unit(rdir), nrm);
+        v3 s;
+        for (;;) {                                           // util.scm:9-15
+            const double a = g.next(), b = g.next(), c = g.next();
+            s = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, c * 2.0 - 1.0);
+            if (dot(s, s) < 1.0) break;
+        }
+        const v3 sd = reflected + s * m.fuzz;
+        if (!(dot(sd, nrm) > 0.0)) return false;             // absorbed: emitted 0
+        const v3 att = tex_value(sc, P, m.tex, pt);
+        p.T = p.T * att;
+        p.d = sd;
+    } else {                                                 // dielectric material.scm:76-101 (R2)
+        const double ref_idx = m.ref_idx;
+        const v3 reflected = reflect(rdir, nrm);
+        const double dd = dot(rdir, nrm);
+        const v3 outward = (dd > 0.0) ? nrm * -1.0 : nrm;
+        const double ni = (dd > 0.0) ? ref_idx : 1.0 / ref_idx;
+        const double cosine = (dd > 0.0) ? (dd * ref_idx) / length(rdir) : (-dd) / length(rdir);
+        // refract :59-67 (raw v in the tangential term, Q5)
+        const v3 uv = unit(rdir);
+        const double dt = dot(uv, outward);
+        const double disc = 1.0 - ni * ni * (1.0 - dt * dt);
+        double prob = 1.0;
+        v3 refracted = mk(0, 0, 0);
+        if (disc > 0.0) {
+            refracted = (rdir - outward * dt) * ni - outward * sqrt(disc);
+            const double r0a = (1.0 - ref_idx) / (1.0 + ref_idx);   // schlick :69-74
+            const double r0 = r0a * r0a;
+            prob = r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
+        }
+        p.d = (g.next() < prob) ? reflected : refracted;   // attenuation (1,1,1)
+    }
+    p.o = pt;
+    p.time = 0.0;                                            // make-ray: time 0 (Q4)
+    p.rng = g.ctr;
+    p.depth += 1u;
+    return true;
+}
+
+__device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
+    if (sc.has_perlin) {   // the Perlin tables (perlin.scm:32-36 data) into LDS
+        for (int k = threadIdx.x; k < 768; k += blockDim.x) { P.ranvec[k] = sc.ranvec[k]; P.perm[k] = sc.perm[k]; }
         __syncthreads();
     }
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    bool alive = false;
-    v3 no = mk(0, 0, 0), nd = mk(0, 0, 0), nT = mk(0, 0, 0);
-    uint32_t pix = 0, smp = 0, wid = 0, rctr = 0, depth = 0;
-    if (i < n) {
-        const v3 ro = mk(in.ox[i], in.oy[i], in.oz[i]);
-        const v3 rdir = mk(in.dx[i], in.dy[i], in.dz[i]);
-        const double time = in.tm[i];
-        const v3 T = mk(in.tr[i], in.tg[i], in.tb[i]);
-        pix = in.pix[i]; smp = in.smp[i]; wid = in.wid[i]; rctr = in.rng[i]; depth = in.depth[i];
-        const double t = hit.t[i];
-        const int32_t leaf = hit.leaf[i];
-        v3 L = mk(0, 0, 0);          // terminal radiance (sky / emission / 0)
-        if (leaf < 0) {
-            if (sc.sky == 0) {       // sky-color main.scm:91-95
-                const v3 ud = unit(rdir);
-                const double s = 0.5 * (1.0 + ud.y);
-                L = mk(1.0, 1.0, 1.0) * (1.0 - s) + mk(0.5, 0.7, 1.0) * s;
-            }
-        } else {
-            const LeafInfo li = sc.leaves[leaf];
-            const Group G = sc.groups[li.group];
-            v3 o = ro, d = rdir;
-            if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
-            v3 p = o + d * t;        // point-at-parameter on the (local) ray
-            v3 nrm;
-            if (li.type == LEAF_SPHERE) {
-                const SphereRec S = sc.sph[li.local];
-                nrm = (p - mk(S.cx, S.cy, S.cz)) * li.inv_r;
-            } else if (li.type == LEAF_MSPHERE) {
-                const MSphereRec S = sc.msph[li.local];
-                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * ((time - S.t0) / S.den);
-                nrm = (p - cen) * li.inv_r;
-            } else if (li.type == LEAF_RECT_XY) {
-                nrm = mk(0.0, 0.0, 1.0);
-            } else if (li.type == LEAF_RECT_XZ) {
-                nrm = mk(0.0, 1.0, 0.0);
-            } else {
-                nrm = mk(1.0, 0.0, 0.0);
-            }
-            if (li.flip) nrm = nrm * -1.0;                          // flip-normals :438
-            if (G.chain >= 0) chain_hit(sc.chains[G.chain], p, nrm);
-            const DevMaterial m = sc.mats[li.mat];
-            Rng g;
-            g.init(rp.k0, rp.k1, pix, smp, rctr);
-            const bool can_continue = depth < (uint32_t)kMaxDepth;
-            // phase 1: scatter direction (all RNG draws, in the reference's order)
-            bool need_tex = false;
-            double wscale = 1.0, ipdf = 1.0;   // lambertian weight: (att*spdf) * (1/pdf)
-            if (m.type == MAT_LAMBERTIAN) {                          // material.scm:24-39
-                if (can_continue) {
-                    // onb.scm:8-16
-                    const v3 axis2 = unit(nrm);
-                    const v3 a = (fabs(axis2.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
-                    const v3 axis1 = unit(cross(axis2, a));
-                    const v3 axis0 = cross(axis2, axis1);
-                    // util.scm:37-44 (x2 quirk on x and y)
-                    const double r1 = g.next();
-                    const double r2 = g.next();
-                    const double z = sqrt(1.0 - r2);
-                    const double phi = 2.0 * kPi * r1;
-                    double sphi, cphi;
-                    sincos(phi, &sphi, &cphi);
-                    const double x = cphi * 2.0 * sqrt(r2);
-                    const double y = sphi * 2.0 * sqrt(r2);
-                    const v3 target = (axis0 * x + axis1 * y) + axis2 * z;   // onb `local`
-                    const v3 sd = unit(target);
-                    const double pdf = dot(axis2, sd) / kPi;
-                    double cosine = dot(nrm, unit(sd));
-                    if (cosine < 0.0) cosine = 0.0;
-                    wscale = cosine / kPi;                           // scattering-pdf
-                    ipdf = 1.0 / pdf;
-                    no = p; nd = sd; alive = true; need_tex = true;
-                }
-            } else if (m.type == MAT_METAL) {                        // material.scm:45-57 (R2)
-                if (can_continue) {
-                    const v3 reflected = reflect(unit(rdir), nrm);
-                    v3 s;
-                    for (;;) {                                       // util.scm:9-15
-                        const double a = g.next(), b = g.next(), c = g.next();
-                        s = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, c * 2.0 - 1.0);
-                        if (dot(s, s) < 1.0) break;
-                    }
-                    const v3 sd = reflected + s * m.fuzz;
-                    if (dot(sd, nrm) > 0.0) { no = p; nd = sd; alive = true; need_tex = true; }
-                }
-            } else if (m.type == MAT_DIELECTRIC) {                   // material.scm:76-101 (R2)
-                if (can_continue) {
-                    const double ref_idx = m.ref_idx;
-                    const v3 reflected = reflect(rdir, nrm);
-                    const double dd = dot(rdir, nrm);
-                    const v3 outward = (dd > 0.0) ? nrm * -1.0 : nrm;
-                    const double ni = (dd > 0.0) ? ref_idx : 1.0 / ref_idx;
-                    const double cosine = (dd > 0.0) ? (dd * ref_idx) / length(rdir) : (-dd) / length(rdir);
-                    // refract :59-67 (raw v in the tangential term, Q5)
-                    const v3 uv = unit(rdir);
-                    const double dt = dot(uv, outward);
-                    const double disc = 1.0 - ni * ni * (1.0 - dt * dt);
-                    double prob = 1.0;
-                    v3 refracted = mk(0, 0, 0);
-                    if (disc > 0.0) {
-                        refracted = (rdir - outward * dt) * ni - outward * sqrt(disc);
-                        const double r0a = (1.0 - ref_idx) / (1.0 + ref_idx);   // schlick :69-74
-                        const double r0 = r0a * r0a;
-                        prob = r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
-                    }
-                    nd = (g.next() < prob) ? reflected : refracted;
-                    no = p; alive = true;                            // attenuation (1,1,1)
-                }
-            } else {                                                 // diffuse light :103-111
-                need_tex = dot(nrm, rdir) < 0.0;
-            }
-            // phase 2: one texture evaluation site (albedo / emission at p)
-            v3 tv = mk(1.0, 1.0, 1.0);
-            if (need_tex) tv = tex_value(sc, P, m.tex, p);
-            // phase 3: throughput (forward form of e + W (*) L_next)
-            if (m.type == MAT_LAMBERTIAN) {
-                nT = mk((T.x * (tv.x * wscale)) * ipdf, (T.y * (tv.y * wscale)) * ipdf,
-                        (T.z * (tv.z * wscale)) * ipdf);
-            } else if (m.type == MAT_METAL) {
-                nT = T * tv;
-            } else if (m.type == MAT_DIELECTRIC) {
-                nT = T;
-            } else if (need_tex) {
-                L = tv;
-            }
-            rctr = g.ctr;
+}
+
+// =====================================================================
+// k_shade<MAT> — one material's queue; survivors compacted into `out`
+// =====================================================================
+template <int MAT>
+__global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderParams rp, const PathState in,
+                                               const HitBuf hit, const uint32_t* __restrict__ queue,
+                                               const QView qv, PathState out, uint32_t* __restrict__ out_counts,
+                                               uint32_t shard_cap) {
+    __shared__ PerlinLds P;
+    __shared__ uint32_t s_cnt[16 + 1];
+    stage_perlin(sc, P);
+    const QMap qm = qmap(qv);
+    uint32_t n = 0;
+#pragma unroll
+    for (int x = 0; x < kShards; ++x) n += qv.counts[x];
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+        const uint32_t k = base + threadIdx.x;
+        bool alive = false;
+        PathRegs p;
+        if (k < n) {
+            const uint32_t i = queue[qphys(qm, k)];
+            load_path(in, i, p);
+            v3 L;
+            alive = shade_hit<MAT>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
+            if (!alive) write_sample(rp, p, L);
         }
-        if (!alive) {                // path done: sample colour = T (*) L
-            rp.sb[wid] = T.x * L.x;
-            rp.sb[rp.B + wid] = T.y * L.y;
-            rp.sb[2u * rp.B + wid] = T.z * L.z;
-        }
+        const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
+        if (alive) store_path(out, slot, p);
     }
-    // stream compaction of survivors: wave64 ballot, mbcnt prefix, one atomic per wave
-    const unsigned long long mask = __ballot(alive);
-    if (mask) {
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        const uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(out_count, (uint32_t)__popcll(mask));
-        base = __shfl(base, (int)leader, 64);
-        if (alive) {
-            const uint32_t k = base + below;
-            out.ox[k] = no.x; out.oy[k] = no.y; out.oz[k] = no.z;
-            out.dx[k] = nd.x; out.dy[k] = nd.y; out.dz[k] = nd.z;
-            out.tm[k] = 0.0;                                         // make-ray: time 0 (Q4)
-            out.tr[k] = nT.x; out.tg[k] = nT.y; out.tb[k] = nT.z;
-            out.pix[k] = pix; out.smp[k] = smp; out.wid[k] = wid; out.rng[k] = rctr;
-            out.depth[k] = depth + 1u;
+}
+
+// =====================================================================
+// k_finish — the long tail (a few dielectric / metal paths bouncing up to
+// depth 100): one thread per remaining path runs extend + shade in a loop
+// instead of ~100 more wavefront launches with a host sync each.
+// =====================================================================
+__global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
+                                                const QView in, uint32_t n,
+                                                unsigned long long* __restrict__ seg_count) {
+    __shared__ PerlinLds P;
+    __shared__ uint32_t s_stack[4 * kBvhStack];
+    __shared__ uint32_t s_lstack[256 * kLaneStack];
+    stage_perlin(sc, P);
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    uint32_t segs = 0;
+    if (k < n) {
+        PathRegs p;
+        load_path(st, qphys(qmap(in), k), p);
+        v3 L;
+        for (;;) {
+            double t;
+            ++segs;
+            const int32_t leaf = closest_hit(sc, p.o, p.d, p.time, t, s_stack + (threadIdx.x >> 6) * kBvhStack,
+                                             s_lstack + threadIdx.x);
+            if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
+            if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
         }
+        write_sample(rp, p, L);
     }
+    // segment statistics: wave sum, one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
+    if ((threadIdx.x & 63u) == 0u && segs) atomicAdd(seg_count, (unsigned long long)segs);
 }
 
 // =====================================================================
@@ -481,17 +739,41 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     hipLaunchKernelGGL(k_raygen, dim3(blocks), dim3(256), 0, s, sc, rp, st);
     return hipGetLastError();
 }
-hipError_t launch_extend(const DevScene& sc, const PathState& st, uint32_t n, const HitBuf& hit,
-                         hipStream_t s) {
+hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
+                         uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
+                         uint32_t* counts, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(k_extend, dim3(blocks), dim3(256), 0, s, sc, st, n, hit);
+    hipLaunchKernelGGL(k_extend, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues, qstride,
+                       shard_cap, counts);
     return hipGetLastError();
 }
-hipError_t launch_shade(const DevScene& sc, const RenderParams& rp, const PathState& in,
-                        const HitBuf& hit, uint32_t n, const PathState& out, uint32_t* out_count,
-                        hipStream_t s) {
+hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
+                        const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
+                        const PathState& out, uint32_t* out_counts, uint32_t shard_cap, hipStream_t s) {
+    uint32_t blocks = (n_upper + 255u) / 256u;
+    blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
+    if (blocks > 4096u) blocks = 4096u;
+    if (blocks == 0u) blocks = kShards;
+    switch (mat) {
+    case MAT_LAMBERTIAN:
+        hipLaunchKernelGGL(k_shade<MAT_LAMBERTIAN>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
+        break;
+    case MAT_METAL:
+        hipLaunchKernelGGL(k_shade<MAT_METAL>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
+        break;
+    case MAT_DIELECTRIC:
+        hipLaunchKernelGGL(k_shade<MAT_DIELECTRIC>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
+        break;
+    default:
+        hipLaunchKernelGGL(k_shade<MAT_DIFFUSE_LIGHT>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
+        break;
+    }
+    return hipGetLastError();
+}
+hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
+                         uint32_t n, unsigned long long* seg_count, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(k_shade, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, n, out, out_count);
+    hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
     return hipGetLastError();
 }
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {

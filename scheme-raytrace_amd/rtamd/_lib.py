@@ -32,6 +32,8 @@ class RtStats(ctypes.Structure):
         ("extend_rays", ctypes.c_uint64),
         ("max_depth_seen", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+        ("ms_finish", ctypes.c_double),
+        ("finish_paths", ctypes.c_uint64),
     ]
 
 

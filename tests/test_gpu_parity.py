@@ -172,3 +172,18 @@ def test_device_resolve_matches_host(gpu_ctx):
          ctypes.c_void_p(out.data_ptr()), None)
     host = gpu.resolve_u8(acc.cpu().numpy(), nx, ny, 4)
     assert np.array_equal(out.cpu().numpy(), host)
+
+
+def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
+    """The wave-uniform BVH only culls: the image equals the brute-force flat
+    list (geometry.scm:33-50) bit for bit."""
+    nx, ny, spp = 64, 40, 4
+    monkeypatch.setenv("RTAMD_BVH_MIN", "1000000000")
+    flat_scene = scenes.random_scene(nx, ny)
+    a = np.zeros(nx * ny * 3)
+    gpu.render_host(flat_scene, nx, ny, 0, spp, SEED, a)
+    monkeypatch.setenv("RTAMD_BVH_MIN", "1")
+    bvh_scene = scenes.random_scene(nx, ny)
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(bvh_scene, nx, ny, 0, spp, SEED, b)
+    assert np.array_equal(a, b)
