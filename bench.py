@@ -28,16 +28,18 @@ sys.path.insert(0, os.path.join(ROOT, "scheme-raytrace_amd"))
 METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector spec (FMA = 2 flops)
-# algorithmic HBM bytes of one extend launch per ray segment:
-# read ray o,d,time (7 x f64 = 56 B), write hit t (8 B) + leaf id (4 B)
-EXTEND_BYTES_PER_SEGMENT = 68
+# Algorithmic HBM bytes of k_extend: every segment reads its
+# ray o,d,time (7 x f64 = 56 B); a hit writes t (8) + leaf id (4) + its queue
+# entry (4) = 16 B; a miss instead reads throughput (24) + work id (4) and
+# writes the sample colour (24) = 52 B.  Misses are counted as one per path
+# (each path ends in the sky except the few absorbed / depth-capped ones), so
+# the figure is an upper bound within ~1%.
+EXTEND_BYTES_PER_SEGMENT = 56 + 16
+EXTEND_BYTES_PER_MISS_EXTRA = 52 - 16
 
 
-def extend_flops_per_segment(n_sph, n_msph):
-    """Algorithmic f64 flops of the brute-force closest-hit loop per segment
-    (non-FMA count): |d|^2 = 5; sphere: oc 3 + b 5 + c 6 + disc 3 = 17;
-    moving sphere: + centre lerp 6 = 23."""
-    return 5 + 17 * n_sph + 23 * n_msph
+def extend_bytes(segments, paths):
+    return EXTEND_BYTES_PER_SEGMENT * segments + EXTEND_BYTES_PER_MISS_EXTRA * paths
 
 
 def parse():
@@ -57,30 +59,31 @@ def parse():
 
 
 def cpu_baseline(scene, nx, ny, seed, budget_s):
-    """Time the oracle (C f64 restatement, OpenMP) on a bounded band of the
-    same frame, 1 spp, growing the band until ~budget_s of CPU work."""
+    """Time the oracle (C f64 restatement, OpenMP over pixels) on a bounded
+    sample of the same workload: a 64-row band of the C2 frame, one spp per
+    call, repeated with successive sample indices until ~budget_s of work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle  # cpu_baseline leg only
     threads = max(1, min(16, os.cpu_count() or 1))
     o = oracle.build_scene(scene)
     acc = np.zeros(nx * ny * 3)
-    rows, t_used, segs_total, rows_done = 4, 0.0, 0, 0
-    y0 = ny // 3
-    while t_used < budget_s and y0 + rows_done + rows <= ny:
-        lo = (y0 + rows_done) * nx
-        hi = lo + rows * nx
+    rows = min(64, ny)
+    y0 = max(0, ny // 3 - rows // 2)
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    t_used, segs_total, passes = 0.0, 0, 0
+    while t_used < budget_s:
         t = time.perf_counter()
-        _, segs = o.render(nx, ny, 0, 1, seed, acc, lo, hi, threads)
+        _, segs = o.render(nx, ny, passes, 1, seed, acc, lo, hi, threads)
         t_used += time.perf_counter() - t
         segs_total += segs
-        rows_done += rows
-        rows *= 2
+        passes += 1
     rate = segs_total / t_used / 1e6
     return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": "oracle/rt_oracle.c (C f64 restatement of the Scheme hot path, OpenMP) on rows %d..%d of "
-                      "the 1920x1080 C2 frame at 1 spp (%d segments, %.1f s); Gauche (the reference runtime) "
-                      "is not installed on the box" % (y0, y0 + rows_done, segs_total, t_used)}
+            "sample": "oracle/rt_oracle.c (C f64 restatement of the Scheme hot path, OpenMP, %d threads) on rows "
+                      "%d..%d of the %dx%d C2 frame, %d spp (%d segments, %.1f s); Gauche, the reference's "
+                      "runtime, is not installed on the box" % (threads, y0, y0 + rows, nx, ny, passes, segs_total,
+                                                                 t_used)}
 
 
 def main():
@@ -123,8 +126,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     segs = paths = 0
-    ms_ext = ms_shade = 0.0
+    ms_ext = ms_shade = ms_fin = 0.0
     launches = 0
+    tail_segs = 0
     for _ in range(a.steps):
         s = step()
         segs += s.segments
@@ -132,6 +136,8 @@ def main():
         ms_ext += s.ms_extend
         ms_shade += s.ms_shade
         launches += s.extend_launches
+        ms_fin += s.ms_finish
+        tail_segs += s.segments - s.extend_rays
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -145,29 +151,35 @@ def main():
     elapsed = float(tmax[0])
     if rank == 0:
         value = segs_all / elapsed / 1e6
-        n_sph = sum(1 for o in scene.obj_list if o.kind == "sphere")
-        n_msph = sum(1 for o in scene.obj_list if o.kind == "moving_sphere")
         roof = None
         valu = None
         if launches and ms_ext > 0:
-            rays_per_launch = segs / launches
+            # wavefront extend launches only (the depth tail runs in k_finish)
+            wf_segs = segs - tail_segs
+            rays_per_launch = wf_segs / launches
             avg_ms = ms_ext / launches
-            achieved = EXTEND_BYTES_PER_SEGMENT * rays_per_launch / (avg_ms * 1e-3) / 1e9
+            bytes_per_launch = extend_bytes(wf_segs, paths) / launches
+            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
             traffic = None
+            pm = None
             pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
             if os.path.exists(pmc):
                 with open(pmc) as f:
                     pm = json.load(f)
-                if pm.get("scene") == a.scene and pm.get("bytes_per_segment"):
-                    traffic = round(pm["bytes_per_segment"] * rays_per_launch)
+                if pm.get("scene") != a.scene or not pm.get("bytes_per_segment"):
+                    pm = None
+            if pm:
+                traffic = round(pm["bytes_per_segment"] * rays_per_launch)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "k_extend", "bytes_per_launch": round(EXTEND_BYTES_PER_SEGMENT * rays_per_launch),
-                    "avg_launch_ms": round(avg_ms, 4)}
-            fl = extend_flops_per_segment(n_sph, n_msph)
-            tf = fl * rays_per_launch / (avg_ms * 1e-3) / 1e12
-            valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4), "flops_per_segment": fl}
+                    "kernel": "k_extend", "bytes_per_launch": round(bytes_per_launch),
+                    "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4)}
+            if pm and pm.get("f64_flops_per_segment"):
+                tf = pm["f64_flops_per_segment"] * rays_per_launch / (avg_ms * 1e-3) / 1e12
+                valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+                        "f64_flops_per_segment": round(pm["f64_flops_per_segment"], 1),
+                        "note": "issued f64 lane-ops from SQ_INSTS_VALU_{ADD,MUL,FMA(x2),TRANS}_F64 x 64"}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
@@ -181,6 +193,7 @@ def main():
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
+            "ms_finish_per_step": round(ms_fin / a.steps, 3),
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, nx, ny, a.seed, a.cpu_baseline_seconds)

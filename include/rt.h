@@ -122,6 +122,12 @@ int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t 
 int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
                      int shard_index, int shard_count, double* accum_device, void* stream);
 
+/* The pixels shard `shard_index` of `shard_count` renders (host-only, no GPU
+ * needed): interleaved 16x16 tiles in row-major tile order, tile t belongs to
+ * shard t % shard_count; pixel j = y*nx + x, listed tile by tile.  Pass
+ * out_pix = NULL to get the count only. */
+int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* out_pix, int64_t* out_count);
+
 /* Statistics of the last render on this scene. */
 typedef struct rt_stats {
     uint64_t segments;    /* closest-hit queries issued by the integrator (ray segments) */

@@ -63,6 +63,10 @@ def lib():
                             ctypes.c_long, ctypes.c_long, ctypes.c_int], ctypes.c_uint64),
             "orc_sample": ([V, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                             ctypes.c_uint32, _dp], None),
+            "orc_render_pixels": ([V, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                   _dp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_long, ctypes.c_int],
+                                  ctypes.c_uint64),
+            "orc_cosine_direction": ([ctypes.c_double, ctypes.c_double, _dp], None),
             "orc_resolve_u8": ([_dp, ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8)], None),
             "orc_philox": ([ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_uint32,
                             ctypes.POINTER(ctypes.c_uint32)], None),
@@ -178,6 +182,12 @@ class OracleScene:
                                  accum.ctypes.data_as(_dp), pix_begin, pix_end, nthreads)
         return accum, segs
 
+    def render_pixels(self, nx, ny, spp_begin, spp_count, seed, accum, pix, nthreads=1):
+        pix = np.ascontiguousarray(pix, dtype=np.uint32)
+        return self.L.orc_render_pixels(self.s, nx, ny, spp_begin, spp_count, seed & (2**64 - 1),
+                                        accum.ctypes.data_as(_dp), pix.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                        pix.size, nthreads)
+
     def sample(self, nx, ny, x, y, seed, smp):
         out = (ctypes.c_double * 3)()
         self.L.orc_sample(self.s, nx, ny, x, y, seed, smp, out)
@@ -252,3 +262,9 @@ def make_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus, t0, t1):
     out = (ctypes.c_double * 24)()
     lib().orc_make_camera(_dv(lookfrom), _dv(lookat), _dv(vup), vfov, aspect, aperture, focus, t0, t1, out)
     return list(out)
+
+
+def cosine_direction(r1, r2):
+    out = (ctypes.c_double * 3)()
+    lib().orc_cosine_direction(r1, r2, out)
+    return tuple(out)

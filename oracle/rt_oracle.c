@@ -675,6 +675,38 @@ uint64_t orc_render(const orc_scene* s, int nx, int ny, int spp_begin, int spp_c
     return total;
 }
 
+/* Same as orc_render for an explicit pixel list (multi-rank tests). */
+uint64_t orc_render_pixels(const orc_scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
+                           double* accum, const uint32_t* pix, long npix, int nthreads) {
+    uint64_t total = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
+#endif
+    for (long q = 0; q < npix; ++q) {
+        const long j = pix[q];
+        int x = (int)(j % nx), y = (int)(j / nx);
+        orc_counters cnt = {0, 0};
+        double r = accum[3 * j], gg = accum[3 * j + 1], b = accum[3 * j + 2];
+        for (int k = 0; k < spp_count; ++k) {
+            v3 c = sample_pixel(s, nx, ny, x, y, seed, (uint32_t)(spp_begin + k), &cnt);
+            r = r + c.x; gg = gg + c.y; b = b + c.z;
+        }
+        accum[3 * j] = r; accum[3 * j + 1] = gg; accum[3 * j + 2] = b;
+        total += cnt.segments;
+    }
+    (void)nthreads;
+    return total;
+}
+
+/* exported KAT helper: util.scm:37-44 with given (r1, r2) */
+void orc_cosine_direction(double r1, double r2, double out[3]) {
+    double z = sqrt(1 - r2);
+    double phi = 2 * ORC_PI * r1;
+    out[0] = cos(phi) * 2 * sqrt(r2);
+    out[1] = sin(phi) * 2 * sqrt(r2);
+    out[2] = z;
+}
+
 /* main.scm:481-491 — correct-gamma of sum/count, then floor(255.99*min(1,c)) */
 void orc_resolve_u8(const double* accum, long npix, int count, uint8_t* out) {
     for (long i = 0; i < 3 * npix; ++i) {

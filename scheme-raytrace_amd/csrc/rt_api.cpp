@@ -1008,6 +1008,16 @@ int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t 
     return 0;
 }
 
+int rt_shard_pixels(int nx, int ny, int shard, int nshard, uint32_t* out_pix, int64_t* out_count) {
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if (nshard <= 0 || shard < 0 || shard >= nshard) return fail("invalid shard index/count");
+    if (!out_count) return fail("null out pointer");
+    const std::vector<uint32_t> pl = make_pixlist(nx, ny, shard, nshard);
+    *out_count = (int64_t)pl.size();
+    if (out_pix && !pl.empty()) std::memcpy(out_pix, pl.data(), pl.size() * sizeof(uint32_t));
+    return 0;
+}
+
 int rt_resolve_u8(const double* accum, int nx, int ny, int count, uint8_t* out) {
     if (!accum || !out) return fail("null buffer");
     if (count <= 0) return fail("sample_count must be positive");

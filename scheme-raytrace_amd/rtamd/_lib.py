@@ -78,6 +78,8 @@ _SIGNATURES = {
     "rt_get_stats": [ctypes.c_int, ctypes.POINTER(RtStats)],
     "rt_set_profiling": [ctypes.c_int, ctypes.c_int],
     "rt_resolve_u8": [_c_double_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_u8_p],
+    "rt_shard_pixels": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
+                        ctypes.POINTER(ctypes.c_int64)],
     "rt_resolve_u8_device": [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p],
 }

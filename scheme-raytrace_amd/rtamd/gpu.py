@@ -170,3 +170,13 @@ def resolve_u8(accum, nx, ny, sample_count):
     call("rt_resolve_u8", a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), nx, ny, int(sample_count),
          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
     return out
+
+
+def shard_pixels(nx, ny, shard, nshard):
+    """rt_shard_pixels: the image pixels (j = y*nx + x) shard `shard` renders."""
+    n = ctypes.c_int64(0)
+    call("rt_shard_pixels", nx, ny, shard, nshard, None, ctypes.byref(n))
+    out = np.zeros(n.value, dtype=np.uint32)
+    call("rt_shard_pixels", nx, ny, shard, nshard, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+         ctypes.byref(n))
+    return out

@@ -1,0 +1,156 @@
+"""Host-side logic that needs no GPU: the C ABI exports, scene construction
+(the reference's scene definitions), descriptor emission, the tile partition
+used for multi-GPU sharding, resolve / PPM output."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from rtamd import _lib, scenes
+from rtamd import scene as g
+from rtamd.rng import HostStream
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "rt.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    decl = _header_functions()
+    assert len(decl) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [d for d in decl if d not in exported]
+    assert not missing, missing
+    assert sorted(_lib.EXPORTED) == decl            # the ctypes binding covers the whole ABI
+
+
+def test_library_loads_and_reports_errors_without_gpu():
+    L = _lib.lib()
+    assert L.rt_abi_version() == 1
+    h = ctypes.c_int(0)
+    assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
+    assert b"invalid context" in L.rt_last_error()
+    with pytest.raises(_lib.RtError):
+        _lib.call("rt_shard_pixels", 4, 4, 5, 2, None, ctypes.byref(ctypes.c_int64()))
+
+
+def test_random_scene_structure():
+    sc = scenes.random_scene(200, 100)
+    objs = sc.obj_list
+    # push! order reversed (main.scm:36-88): metal (4,1,0) first, ground last
+    assert objs[0].kind == "sphere" and objs[0].args[0] == (4.0, 1.0, 0.0) and objs[0].args[2].kind == "metal"
+    assert objs[1].args[0] == (-4.0, 1.0, 0.0) and objs[2].args[2].kind == "dielectric"
+    assert objs[-1].args[0] == (0.0, -1000.0, 0.0) and objs[-1].args[1] == 1000.0
+    small = objs[3:-1]
+    assert 150 <= len(small) <= 225
+    for o in small:
+        c = o.args[0]
+        assert c[1] == 0.2
+        assert ((c[0] - 4) ** 2 + (c[2]) ** 2) ** 0.5 > 0.9     # skip test main.scm:49
+        if o.kind == "moving_sphere":
+            assert o.args[2] == 0.0 and o.args[3] == 1.0 and o.args[4] == 0.2
+            assert 0.0 <= o.args[1][1] - 0.2 <= 0.5
+            assert o.args[5].kind == "lambertian"
+        else:
+            assert o.args[1] == 0.2 and o.args[2].kind in ("metal", "dielectric")
+    # deterministic in the host seed, different for another
+    again = scenes.random_scene(200, 100).obj_list
+    assert [o.args[0] for o in again] == [o.args[0] for o in objs]
+    other = scenes.random_scene(200, 100, seed=1).obj_list
+    assert [o.args[0] for o in other] != [o.args[0] for o in objs]
+
+
+def test_random_scene_draw_order():
+    """First grid cell: choose-mat, then centre x, then centre z (main.scm:45-48)."""
+    rr = HostStream(scenes.SCENE_SEED)
+    choose, cx, cz = rr(), rr(), rr()
+    center = (-5 + 0.9 * cx, 0.2, -5 + 0.9 * cz)
+    small_last = scenes.random_scene(10, 10).obj_list[-2]      # first pushed small sphere
+    assert small_last.args[0] == center
+    assert small_last.kind == ("moving_sphere" if choose < 0.8 else "sphere")
+
+
+class Recorder:
+    """A builder that records the descriptor stream (scene.emit)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def __getattr__(self, name):
+        def f(*a):
+            self.calls.append((name, a))
+            return len(self.calls) - 1
+        return f
+
+
+def test_emit_shares_objects_and_orders_children_first():
+    sc = scenes.cornell_box(64, 64)
+    r = Recorder()
+    g.emit(sc, r)
+    names = [c[0] for c in r.calls]
+    assert names.count("material_lambertian") == 3 and names.count("material_diffuse_light") == 1
+    assert names.count("box") == 2 and names.count("rotate_y") == 2 and names.count("translate") == 2
+    assert names[-4:] == ["list", "set_camera", "set_sky", "commit"]
+    # every referenced id was produced earlier
+    for i, (name, args) in enumerate(r.calls):
+        for a in args:
+            if isinstance(a, int) and name not in ("rect", "set_sky"):
+                assert a < i
+
+
+def test_emit_requires_perlin_tables():
+    sc = scenes.test_scene2(8, 8)
+    sc.perlin = None
+    with pytest.raises(ValueError):
+        g.emit(sc, Recorder())
+
+
+def test_constructor_type_checks():
+    with pytest.raises(TypeError):
+        g.make_sphere((0, 0, 0), 1, "not a material")
+    with pytest.raises(TypeError):
+        g.make_scene([], None, lambda r: None)
+
+
+@pytest.mark.parametrize("nx,ny,n", [(1920, 1080, 8), (33, 17, 3), (16, 16, 2), (5, 3, 4)])
+def test_shard_partition_is_exact(nx, ny, n):
+    from rtamd import gpu
+    parts = [gpu.shard_pixels(nx, ny, r, n) for r in range(n)]
+    allpix = np.concatenate(parts)
+    assert allpix.size == nx * ny
+    assert np.array_equal(np.sort(allpix), np.arange(nx * ny, dtype=np.uint32))
+    # tile t -> shard t % n (16x16 tiles, row-major)
+    tx = (nx + 15) // 16
+    for r, p in enumerate(parts):
+        x, y = p % nx, p // nx
+        assert np.all(((y // 16) * tx + x // 16) % n == r)
+
+
+def test_resolve_matches_reference_formula(oracle_mod):
+    from rtamd import gpu
+    rs = np.random.RandomState(3)
+    acc = rs.uniform(0, 5, size=7 * 5 * 3)
+    acc[:5] = [0.0, 4.0, 4.0000001, 1e-9, 100.0]
+    want = np.array([int(np.floor(255.99 * min(1.0, np.sqrt(a / 4)))) for a in acc], dtype=np.uint8)
+    assert np.array_equal(gpu.resolve_u8(acc, 7, 5, 4), want)
+    assert np.array_equal(oracle_mod.resolve_u8(acc, 4), want)
+
+
+def test_ppm_writer_flips_rows(tmp_path):
+    from rtamd.render import write_ppm
+    img = np.arange(2 * 3 * 3, dtype=np.uint8)        # nx=2, ny=3, y-up rows
+    p = tmp_path / "t.ppm"
+    write_ppm(str(p), img, 2, 3)
+    lines = p.read_text().splitlines()
+    assert lines[0] == "P3" and lines[1] == " 2 3" and lines[2] == "255"   # main.scm:442
+    assert lines[3] == "12 13 14"                     # top row first = y = ny-1 (main.scm:445)
+    assert lines[-1] == "3 4 5"
