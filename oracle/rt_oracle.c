@@ -566,7 +566,14 @@ static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters
     switch (m->type) {
     case MAT_LAMBERTIAN: {                                              /* material.scm:24-39 */
         onb_t uvw = make_onb_from_w(rec.n);
-        v3 target = onb_local(uvw, random_cosine_direction(g));
+        /* (local uvw (random-cosine-direction)) — `local` is a syntax-rules
+         * macro (onb.scm:27-36) that substitutes its argument EXPRESSION into
+         * (v:x a), (v:y a) and (v:z a): random-cosine-direction runs three
+         * times, left to right, and each call contributes one component (Q29). */
+        double cx = random_cosine_direction(g).x;
+        double cy = random_cosine_direction(g).y;
+        double cz = random_cosine_direction(g).z;
+        v3 target = onb_local(uvw, V(cx, cy, cz));
         ray_t scattered = {rec.p, vunit(target), 0.0};
         v3 att = tex_value(s, m->tex, 0, 0, rec.p);
         double pdf = vdot(uvw.w, scattered.d) / ORC_PI;

@@ -572,15 +572,17 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         const v3 a = (fabs(axis2.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
         const v3 axis1 = unit(cross(axis2, a));
         const v3 axis0 = cross(axis2, axis1);
-        // util.scm:37-44 (x2 quirk on x and y)
-        const double r1 = g.next();
-        const double r2 = g.next();
-        const double z = sqrt(1.0 - r2);
-        const double phi = 2.0 * kPi * r1;
-        double sphi, cphi;
-        sincos(phi, &sphi, &cphi);
-        const double x = cphi * 2.0 * sqrt(r2);
-        const double y = sphi * 2.0 * sqrt(r2);
+        // (local uvw (random-cosine-direction)): `local` is a syntax-rules
+        // macro (onb.scm:27-36), so random-cosine-direction (util.scm:37-44,
+        // x2 quirk on x and y) runs three times, left to right, and call k
+        // supplies component k only (Q29): 6 draws, the 5th unused.
+        const double r1 = g.next(), r2 = g.next();
+        const double r3 = g.next(), r4 = g.next();
+        (void)g.next();
+        const double r6 = g.next();
+        const double x = cos(2.0 * kPi * r1) * 2.0 * sqrt(r2);
+        const double y = sin(2.0 * kPi * r3) * 2.0 * sqrt(r4);
+        const double z = sqrt(1.0 - r6);
         const v3 target = (axis0 * x + axis1 * y) + axis2 * z;   // onb `local`
         const v3 sd = unit(target);
         const double pdf = dot(axis2, sd) / kPi;

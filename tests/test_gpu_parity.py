@@ -187,3 +187,23 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     b = np.zeros(nx * ny * 3)
     gpu.render_host(bvh_scene, nx, ny, 0, spp, SEED, b)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah"])
+def test_gpu_vs_reference_fixtures(name, gpu_ctx):
+    """The GPU against the outputs of the REFERENCE's own source, executed
+    (tests/golden/make_golden.py): same scene, seed and streams."""
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_%s.json" % name)
+    with open(path) as f:
+        g = json.load(f)
+    nx, ny, spp = g["nx"], g["ny"], g["spp"]
+    want = np.array([float.fromhex(v) for px in g["accum"] for v in px])
+    acc = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.SCENES[name](nx, ny), nx, ny, 0, spp, g["path_seed"], acc)
+    rms, dmax, nbad, npx = _compare(acc, want, spp)
+    print("%s vs reference: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (name, rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 100)
+    img = gpu.resolve_u8(acc, nx, ny, spp)
+    assert (np.abs(img.astype(int) - np.array(g["image"])) <= 1).all()
