@@ -366,6 +366,7 @@ int commit_scene(Scene* s, int world) {
     std::vector<BvhNode2> bvh2;
     std::vector<BvhLeaf> bleaf;
     int32_t bvh2_root = 0;
+    int32_t lane_stack = 0;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         bb.build(0, (int)refs.size(), 0);
@@ -399,6 +400,11 @@ int commit_scene(Scene* s, int world) {
             M.l = ref_of(bvh_nodes[i].a); M.r = ref_of(bvh_nodes[i].b);
         }
         bvh2_root = ref_of(0);
+        // stack entries a per-lane traversal can need = depth of the BVH2
+        std::vector<int> depth(bvh_nodes.size(), 0);
+        for (size_t i = 0; i < bvh_nodes.size(); ++i)
+            if (bvh_nodes[i].c < 0) { depth[bvh_nodes[i].a] = depth[i] + 1; depth[bvh_nodes[i].b] = depth[i] + 1; }
+        for (int dd : depth) lane_stack = std::max(lane_stack, dd);
         const int gid = (int)groups.size();
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
@@ -494,6 +500,8 @@ int commit_scene(Scene* s, int world) {
     d.n_bvh2 = (int)bvh2.size();
     d.bvh2_root = bvh2_root;
     d.traversal = traversal_mode();
+    d.lane_stack = lane_stack;
+    if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
     if (int rc = upload(s->d_leaves, leaves, &d.leaves)) return rc;
     if (int rc = upload(s->d_mats, s->mats, &d.mats)) return rc;

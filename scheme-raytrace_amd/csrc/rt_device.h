@@ -58,6 +58,7 @@ constexpr int kBvhStack = 64;                  // per-wave traversal stack (LDS)
 struct alignas(16) BvhNode2 { double lbox[6]; double rbox[6]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn; };       // spheres [sb,sb+sn), moving [mb,mb+mn)
 constexpr int kLaneStack = 32;                 // per-lane traversal stack (LDS, stride = block size)
+constexpr int kLaneStackSmall = 12;            // kernel variant for BVHs at most 12 levels deep
 enum Traversal : int32_t { TRAV_WAVE = 0, TRAV_LANE = 1 };
 
 // Shade-side per-leaf record (indexed by leaf id).
@@ -89,6 +90,7 @@ struct DevScene {
     const BvhNode2* bvh2;  int32_t n_bvh2;
     const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)
     int32_t traversal;                             // Traversal
+    int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
     int32_t leaf_base[5];                      // first leaf id of each LeafType

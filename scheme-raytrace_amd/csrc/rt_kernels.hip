@@ -235,7 +235,7 @@ __device__ __forceinline__ bool box_hit_t(const double* bx, const v3 o, const v3
 }
 
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
-                                                 double& closest, int32_t& best, uint32_t* lstk) {
+                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
     const double a = dot(d, d);
     const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
@@ -250,7 +250,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             const bool hr = box_hit_t(N.rbox, o, inv, closest, tr);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
-                if (sp < kLaneStack) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
                 node = lfirst ? N.l : N.r;
                 continue;
             }
@@ -282,13 +282,13 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 // fetched once per wave through the scalar unit.
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
                                                const double time, double& closest, uint32_t* stk,
-                                               uint32_t* lstk) {
+                                               uint32_t* lstk, const int lmax) {
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
         const Group G = sc.groups[g];
         if (G.type == GROUP_BVH) {
-            if (sc.traversal == TRAV_LANE) bvh_closest_lane(sc, o0, d0, time, closest, best, lstk);
+            if (sc.traversal == TRAV_LANE) bvh_closest_lane(sc, o0, d0, time, closest, best, lstk, lmax);
             else bvh_closest(sc, o0, d0, time, closest, best, stk);
             continue;
         }
@@ -428,12 +428,13 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
 // the spot (sky); hits are appended to the queue of their material type so
 // each shade kernel runs one material's code (wavefront material queues).
 // =====================================================================
+template <int LS>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                 uint32_t* __restrict__ queues, uint32_t qstride,
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts) {
     __shared__ uint32_t s_stack[4 * kBvhStack];
-    __shared__ uint32_t s_lstack[256 * kLaneStack];
+    __shared__ uint32_t s_lstack[256 * LS];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     int cls = -1;
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
         double t;
         const int32_t leaf = closest_hit(sc, o, d, st.tm[i], t, s_stack + (threadIdx.x >> 6) * kBvhStack,
-                                         s_lstack + threadIdx.x);
+                                         s_lstack + threadIdx.x, LS);
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             const uint32_t wid = st.wid[i];
@@ -679,12 +680,13 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
+template <int LS>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ seg_count) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_stack[4 * kBvhStack];
-    __shared__ uint32_t s_lstack[256 * kLaneStack];
+    __shared__ uint32_t s_lstack[256 * LS];
     stage_perlin(sc, P);
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     uint32_t segs = 0;
@@ -696,7 +698,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
             double t;
             ++segs;
             const int32_t leaf = closest_hit(sc, p.o, p.d, p.time, t, s_stack + (threadIdx.x >> 6) * kBvhStack,
-                                             s_lstack + threadIdx.x);
+                                             s_lstack + threadIdx.x, LS);
             if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
             if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
         }
@@ -745,8 +747,12 @@ hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathS
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
                          uint32_t* counts, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(k_extend, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues, qstride,
-                       shard_cap, counts);
+    if (sc.lane_stack <= kLaneStackSmall)
+        hipLaunchKernelGGL(k_extend<kLaneStackSmall>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,
+                           qstride, shard_cap, counts);
+    else
+        hipLaunchKernelGGL(k_extend<kLaneStack>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,
+                           qstride, shard_cap, counts);
     return hipGetLastError();
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
@@ -775,7 +781,10 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, unsigned long long* seg_count, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
+    if (sc.lane_stack <= kLaneStackSmall)
+        hipLaunchKernelGGL(k_finish<kLaneStackSmall>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
+    else
+        hipLaunchKernelGGL(k_finish<kLaneStack>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
     return hipGetLastError();
 }
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtamd.so")
+# RTAMD_LIB selects an alternative in-tree build (e.g. an A/B variant)
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(_HERE, "librtamd.so")
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _c_double_p = ctypes.POINTER(ctypes.c_double)
