@@ -86,6 +86,16 @@ def cpu_baseline(scene, nx, ny, seed, budget_s):
                                                                  t_used)}
 
 
+SCENE_CONFIG = {"cover": "C2", "cover_marble": "C3", "cornell": "C4", "curves": "C5"}
+SCENE_DATA = {
+    "cover": "RTIOW cover scene (random-scene, main.scm:31-89 + repairs R1/R3) generated from host seed 0x5EED0001",
+    "cover_marble": "cover scene with a marble ground (C3), host seed 0x5EED0001, Perlin seed 0x5EED0003",
+    "cornell": "cornell-box (main.scm:330-351)",
+    "curves": "2^20 curves from seeded random polylines via points->bezier (numpy seed 0x5EED0005) in a BVH "
+              "inside the cornell-bezier frame (main.scm:353-373)",
+}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -184,9 +194,9 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: RTIOW cover scene (random-scene, main.scm:31-89 + repairs R1/R3) generated "
-                    "from host seed 0x5EED0001; path RNG seed %#x" % a.seed,
-            "config": {"workload": "C2: %s scene %dx%dx%dspp, one full frame per step" % (a.scene, nx, ny, spp),
+            "data": "synthetic: %s; path RNG seed %#x" % (SCENE_DATA.get(a.scene, a.scene + " scene"), a.seed),
+            "config": {"workload": "%s: %s scene %dx%dx%dspp, one full frame per step"
+                                   % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp),
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
             "roofline": roof, "valu": valu,

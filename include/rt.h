@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -77,6 +77,13 @@ int rt_add_moving_sphere(int scene, const double center0[3], const double center
 /* axis: RT_RECT_XY (a=x,b=y,k=z), RT_RECT_XZ (a=x,b=z,k=y), RT_RECT_YZ (a=y,b=z,k=x) */
 int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1, double k,
                 int mat, int* out_obj);                                                          /* g:make-{xy,xz,yz}-rect :376-431 */
+/* cubic Bezier curve a,b,c,d of the given width (b:make-bezier bezier.scm:61); hit t is the distance
+ * along unit(dir) and the normal is -dir (bezier.scm:176-214) */
+int rt_add_bezier(int scene, const double a[3], const double b[3], const double c[3], const double d[3],
+                  double width, int mat, int* out_obj);
+/* n curves at once (bezier->objs points.scm:45-53 over points->bezier output): cps holds n*12 doubles
+ * (a,b,c,d per curve); the curves get the consecutive object ids *out_first .. *out_first + n - 1 */
+int rt_add_bezier_array(int scene, const double* cps, int n, double width, int mat, int* out_first);
 int rt_add_flip_normals(int scene, int obj, int* out_obj);                                       /* g:flip-normals :433 */
 int rt_add_box(int scene, const double p0[3], const double p1[3], int mat, int* out_obj);       /* g:make-box :444 */
 int rt_add_translate(int scene, int obj, const double offset[3], int* out_obj);                 /* g:translate :465 */

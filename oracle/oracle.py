@@ -47,6 +47,8 @@ def lib():
             "orc_add_rect": ([V, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, ctypes.c_double, ctypes.c_int], ctypes.c_int),
             "orc_add_flip_normals": ([V, ctypes.c_int], ctypes.c_int),
+            "orc_add_bezier": ([V, _dp, ctypes.c_double, ctypes.c_int], ctypes.c_int),
+            "orc_add_bezier_array": ([V, _dp, ctypes.c_int, ctypes.c_double, ctypes.c_int], ctypes.c_int),
             "orc_add_box": ([V, _dp, _dp, ctypes.c_int], ctypes.c_int),
             "orc_add_translate": ([V, ctypes.c_int, _dp], ctypes.c_int),
             "orc_add_rotate_y": ([V, ctypes.c_int, ctypes.c_double], ctypes.c_int),
@@ -141,6 +143,14 @@ class OracleScene:
 
     def flip_normals(self, o):
         return self.L.orc_add_flip_normals(self.s, o)
+
+    def bezier_array(self, cps, width, mat):
+        import numpy as np
+        arr = np.ascontiguousarray(cps, dtype=np.float64)
+        return self.L.orc_add_bezier_array(self.s, arr.ctypes.data_as(_dp), int(arr.shape[0]), width, mat)
+
+    def bezier(self, a, b, c, d, width, mat):
+        return self.L.orc_add_bezier(self.s, _dv(list(a) + list(b) + list(c) + list(d)), width, mat)
 
     def box(self, p0, p1, mat):
         return self.L.orc_add_box(self.s, _dv(p0), _dv(p1), mat)

@@ -112,7 +112,7 @@ static inline v3 point_at(ray_t r, double t) { return vadd(r.o, vscale(r.d, t));
 enum { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum { OBJ_SPHERE = 0, OBJ_MOVING_SPHERE, OBJ_RECT, OBJ_FLIP, OBJ_BOX, OBJ_TRANSLATE,
-       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH };
+       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH, OBJ_BEZIER };
 
 typedef struct { int type, a, b; v3 rgb; double scale; } orc_tex;
 typedef struct { int type, tex; double fuzz, ref_idx; } orc_mat;
@@ -124,6 +124,8 @@ typedef struct {
     double a0, a1, b0, b1, k;           /* rect */
     double sin_t, cos_t;                /* rotate-y */
     int box_list;                       /* OBJ_BOX: its 6-rect list object */
+    v3 cp[4];                           /* OBJ_BEZIER control points */
+    double width;
 } orc_obj;
 
 typedef struct {
@@ -259,6 +261,22 @@ int orc_add_rotate_y(orc_scene* s, int child, double angle) {
     s->obj[i].mat = s->obj[child].mat;
     return i;
 }
+int orc_add_bezier(orc_scene* s, const double* cps, double width, int mat) {
+    int i = new_obj(s, OBJ_BEZIER);
+    for (int k = 0; k < 4; ++k) s->obj[i].cp[k] = V(cps[3 * k], cps[3 * k + 1], cps[3 * k + 2]);
+    s->obj[i].width = width; s->obj[i].mat = mat;
+    return i;
+}
+
+int orc_add_bezier_array(orc_scene* s, const double* cps, int n, double width, int mat) {
+    int first = -1;
+    for (int i = 0; i < n; ++i) {
+        int id = orc_add_bezier(s, cps + 12 * (size_t)i, width, mat);
+        if (i == 0) first = id;
+    }
+    return first;
+}
+
 void orc_set_camera(orc_scene* s, const double cam[24]) { memcpy(s->cam, cam, sizeof s->cam); }
 void orc_set_sky(orc_scene* s, int sky) { s->sky = sky; }
 void orc_set_world(orc_scene* s, int world) { s->world = world; }
@@ -393,6 +411,150 @@ static v3 tex_value(const orc_scene* s, int id, double u, double v, v3 p) {
 /* --------------------------------------------------------- geometry.scm */
 typedef struct { double t; v3 p, n; int mat; double u, v; } hitrec;
 
+/* ------------------------------------------------------------ bezier.scm */
+/* A cubic Bezier curve of a given width (bezier.scm:61-223). */
+typedef struct { v3 p[4]; } bez4;
+
+static v3 bez_point(const bez4* c, double t) {                          /* bez-p :67-77 */
+    double t2 = t * t, t3 = t2 * t;
+    double u = 1 - t, u2 = u * u, u3 = u2 * u;
+    return vadd(vadd(vadd(vscale(c->p[0], u3), vscale(c->p[1], 3 * u2 * t)), vscale(c->p[2], 3 * u * t2)),
+                vscale(c->p[3], t3));
+}
+static v3 idiv(v3 a, v3 b, double t) { return vadd(vscale(a, 1 - t), vscale(b, t)); }   /* :45-47 */
+static void bez_split(const bez4* c, double t, bez4* l, bez4* r) {      /* split :78-87 */
+    v3 sp = bez_point(c, t);
+    v3 nbc = idiv(c->p[1], c->p[2], t);
+    v3 lb = idiv(c->p[0], c->p[1], t);
+    v3 lc = idiv(lb, nbc, t);
+    v3 rc = idiv(c->p[2], c->p[3], t);
+    v3 rb = idiv(nbc, rc, t);
+    l->p[0] = c->p[0]; l->p[1] = lb; l->p[2] = lc; l->p[3] = sp;
+    r->p[0] = sp; r->p[1] = rb; r->p[2] = rc; r->p[3] = c->p[3];
+}
+/* bez-tan-vec :106-117 (t is the exact integer 0 or 1 at its call sites) */
+static v3 bez_tan(const bez4* c, int t) {
+    const v3 a = c->p[0], b = c->p[1], cc = c->p[2], d = c->p[3];
+    v3 coef_a = vadd(vadd(vadd(vscale(b, 3), d), vscale(cc, -3)), vscale(a, -1));
+    v3 coef_b = vscale(vadd(vadd(a, vscale(b, -2)), cc), 3);
+    v3 coef_c = vscale(vsub(b, a), 3);
+    double t2 = (double)(t * t);
+    return vunit(vadd(vadd(vscale(coef_a, 3 * t2), vscale(coef_b, 2 * t)), coef_c));
+}
+static double dot2d(v3 a, v3 b) { return vdot(V(a.x, a.y, 0), V(b.x, b.y, 0)); }   /* :57-59 */
+
+/* get-projection-mat :13-43, as a 4x4 row-major matrix M (array-mul of the
+ * translation and the rotation: s = 0; s += T[i][k]*R[k][j], k = 0..3) */
+static void projection_mat(ray_t r, double M[16]) {
+    double ox = -r.o.x, oy = -(-r.o.z), oz = -r.o.y;
+    v3 rd = vunit(r.d);
+    double lx = rd.x, ly = -rd.z, lz = rd.y;
+    double d = sqrt(lx * lx + lz * lz);
+    double R[16];
+    if (d == 0) {
+        double angle = (ly >= 0) ? -(ORC_PI / 2) : (ORC_PI / 2);
+        double cs = cos(angle), sn = sin(angle);
+        double Rr[16] = {1, 0, 0, 0, 0, cs, -sn, 0, 0, sn, cs, 0, 0, 0, 0, 1};
+        memcpy(R, Rr, sizeof R);
+    } else {
+        double Rr[16] = {lz / d, (-1 * lx * ly) / d, lx, 0, 0, d, ly, 0,
+                         (-lx) / d, (-1 * ly * lz) / d, lz, 0, 0, 0, 0, 1};
+        memcpy(R, Rr, sizeof R);
+    }
+    double T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, ox, oy, oz, 1};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double sum = 0;
+            for (int k = 0; k < 4; ++k) sum = sum + T[4 * i + k] * R[4 * k + j];
+            M[4 * i + j] = sum;
+        }
+}
+/* transform :49-55 — row vector (x, -z, y, 1) times M */
+static v3 bez_transform(v3 p, const double M[16]) {
+    double row[4] = {p.x, -p.z, p.y, 1};
+    double out[3];
+    for (int j = 0; j < 3; ++j) {
+        double sum = 0;
+        for (int k = 0; k < 4; ++k) sum = sum + row[k] * M[4 * k + j];
+        out[j] = sum;
+    }
+    return V(out[0], out[1], out[2]);
+}
+
+/* converge :121-175.  Both children of a split see the t the parent was
+ * called with, so the recursion returns min z over every leaf hit with
+ * z <= t_entry; *found tells whether any leaf hit. */
+static void bez_converge(const bez4* c, int depth, double v0, double vn, double t, double width1,
+                         double width2, int* found, double* best) {
+    double mn[3] = {ORC_TMAX, ORC_TMAX, ORC_TMAX}, mx[3] = {-ORC_TMAX, -ORC_TMAX, -ORC_TMAX};
+    for (int i = 0; i < 4; ++i) {                                  /* bbox :88-98 */
+        double pc[3] = {c->p[i].x, c->p[i].y, c->p[i].z};
+        for (int a = 0; a < 3; ++a) {
+            double lo = pc[a] - width1, hi = pc[a] + width1;
+            mn[a] = (lo < mn[a]) ? lo : mn[a];
+            mx[a] = (hi > mx[a]) ? hi : mx[a];
+        }
+    }
+    if (mn[2] >= t || mx[2] <= 0.000001 || mn[0] >= width1 || mx[0] <= -width1 || mn[1] >= width1 ||
+        mx[1] <= -width1)
+        return;
+    if (depth < 0) {                                               /* leaf :130-166 */
+        v3 dir = vsub(c->p[3], c->p[0]);
+        v3 dp0 = bez_tan(c, 0);
+        if (dot2d(dir, dp0) < 0) dp0 = vscale(dp0, -1);
+        if (dot2d(dp0, vscale(c->p[0], -1)) < 0) return;
+        v3 dpn = bez_tan(c, 1);
+        if (dot2d(dir, dpn) < 0) dpn = vscale(dpn, -1);
+        if (dot2d(dpn, c->p[3]) < 0) return;
+        double w = dir.x * dir.x + dir.y * dir.y;
+        if (w == 0) return;
+        w = (c->p[0].x * dir.x + c->p[0].y * dir.y) / (-w);
+        w = (w < 0) ? 0 : ((w > 1) ? 1 : w);                       /* clamp */
+        double v = v0 * (1 - w) + vn * w;
+        v3 p = bez_point(c, v);                                    /* sub-curve at the global v (Q11) */
+        if (p.x * p.x + p.y * p.y >= width2 || p.z <= 0.0001 || t < p.z) return;
+        if (!*found || p.z < *best) *best = p.z;
+        *found = 1;
+        return;
+    }
+    double vm = (v0 + vn) / 2;
+    bez4 l, r;
+    bez_split(c, 0.5, &l, &r);
+    bez_converge(&l, depth - 1, v0, vm, t, width1, width2, found, best);
+    bez_converge(&r, depth - 1, vm, vn, t, width1, width2, found, best);
+}
+
+/* hit :176-214 */
+static int bezier_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitrec* rec) {
+    double width1 = o->width / 2, width2 = width1 * width1, eps = o->width / 20;
+    double M[16];
+    projection_mat(r, M);
+    bez4 c;
+    for (int k = 0; k < 4; ++k) c.p[k] = bez_transform(o->cp[k], M);
+    double l0 = -ORC_TMAX;
+    for (int i = 0; i < 2; ++i) {
+        double x = fabs(c.p[i].x + -2 * c.p[i + 1].x + c.p[i + 2].x);
+        double y = fabs(c.p[i].y + -2 * c.p[i + 1].y + c.p[i + 2].y);
+        double m = x;
+        if (y > m) m = y;
+        if (l0 > m) m = l0;
+        l0 = m;
+    }
+    double md = log((sqrt(2) * 4 * 3 * l0) / (8 * eps)) / log(4);
+    int max_depth = (md == -INFINITY) ? 0 : (int)ceil(md);
+    int found = 0;
+    double t = tmax;
+    bez_converge(&c, max_depth, 0, 1, tmax, width1, width2, &found, &t);
+    if (!found) t = tmax;
+    if (!(found && tmin < t)) return 0;
+    rec->t = t;
+    rec->p = point_at(r, t);                 /* t is a ray-space distance used on the raw ray (Q10) */
+    rec->n = vscale(r.d, -1);                /* un-normalised (Q12) */
+    rec->mat = o->mat;
+    rec->u = 0; rec->v = 0;
+    return 1;
+}
+
 static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec);
 
 static int hit_list(const orc_scene* s, int first, int count, ray_t r, double tmin, double tmax,
@@ -488,6 +650,8 @@ static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax
     case OBJ_LIST:
     case OBJ_BVH:
         return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
+    case OBJ_BEZIER:
+        return bezier_hit(o, r, tmin, tmax, rec);
     }
     return 0;
 }

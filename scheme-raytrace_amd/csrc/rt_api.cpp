@@ -45,7 +45,7 @@ int fail(const std::string& msg) { g_err = msg; return 1; }
     } while (0)
 
 // ------------------------------------------------------------- objects
-enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH };
+enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH, O_BEZIER };
 
 struct Obj {
     ObjType type;
@@ -55,6 +55,8 @@ struct Obj {
     double r = 0, t0 = 0, t1 = 0;
     double a0 = 0, a1 = 0, b0 = 0, b1 = 0, k = 0;
     double sin_t = 0, cos_t = 1;
+    double cp[12] = {0};       // O_BEZIER control points a, b, c, d
+    double width = 0;
 };
 
 struct DevBuf {
@@ -92,7 +94,7 @@ struct Scene {
 
     // flattened + uploaded
     DevScene dev{};
-    DevBuf d_sph, d_msph, d_rect, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh, d_bvh2, d_bleaf;
+    DevBuf d_sph, d_msph, d_rect, d_bez, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     // render buffers
     DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
     uint32_t* h_counts = nullptr;     // pinned
@@ -174,6 +176,7 @@ struct Flattener {
         case O_SPHERE: leaves.push_back({LEAF_SPHERE, chain_id(), flip, id}); break;
         case O_MSPHERE: leaves.push_back({LEAF_MSPHERE, chain_id(), flip, id}); break;
         case O_RECT: leaves.push_back({LEAF_RECT_XY + o.axis, chain_id(), flip, id}); break;
+        case O_BEZIER: leaves.push_back({LEAF_BEZIER, chain_id(), flip, id}); break;
         case O_FLIP: rc = walk(o.child, flip ^ 1); break;
         case O_BOX:
         case O_LIST:
@@ -198,13 +201,16 @@ struct Flattener {
 };
 
 // ------------------------------------------------------------------ BVH
-// Binned-SAH BVH over the world-level spheres / moving spheres, traversed
-// wave-uniformly by k_extend (rt_kernels.hip bvh_closest).  Boxes are padded
-// outward (relative 1e-8) so culling is conservative and the closest hit is
-// exactly the flat list's (geometry.scm:33-50), ties aside.  Moving spheres
-// are bounded over every time a ray can carry: camera rays in [time0, time1],
-// scattered rays at 0 (Q4, Q13).
-struct PrimRef { double lo[3], hi[3], c[3]; int leaf; bool moving; };
+// Binned-SAH BVH over the world-level spheres / moving spheres / curves,
+// traversed per lane by k_extend (rt_kernels.hip bvh_closest_lane).  Boxes are
+// padded outward (relative 1e-8) so culling is conservative and the closest
+// hit is exactly the flat list's (geometry.scm:33-50), ties aside.  Moving
+// spheres are bounded over every time a ray can carry: camera rays in
+// [time0, time1], scattered rays at 0 (Q4, Q13); curves by their control
+// points +- width/2 (bezier.scm:88-98).
+struct PrimRef { double lo[3], hi[3], c[3]; int leaf; int type; };
+// build-time node: inner c = -1, a/b = children, d = split axis; leaf c = -2, refs [a, b)
+struct BvhNode { double lo[3], hi[3]; int32_t a, b, c, d; };
 
 struct BvhBuild {
     std::vector<PrimRef>& refs;
@@ -289,12 +295,6 @@ void pad_box(double* lo, double* hi) {
     for (int k = 0; k < 3; ++k) { lo[k] -= pad; hi[k] += pad; }
 }
 
-int traversal_mode() {
-    const char* e = std::getenv("RTAMD_TRAVERSAL");
-    if (e && std::strcmp(e, "wave") == 0) return TRAV_WAVE;
-    return TRAV_LANE;
-}
-
 size_t bvh_min_prims() {
     const char* e = std::getenv("RTAMD_BVH_MIN");
     return e ? (size_t)std::strtoull(e, nullptr, 10) : 16;
@@ -330,18 +330,35 @@ int commit_scene(Scene* s, int world) {
     std::vector<Group> groups;
     std::vector<LeafInfo> lsph, lmsph, lrect[3];
 
-    // BVH over the world-level (chain -1) spheres and moving spheres
+    std::vector<BezierRec> bez;
+    std::vector<LeafInfo> lbez;
+    auto bezier_rec = [](const Obj& o) {
+        BezierRec b{};
+        for (int k = 0; k < 12; ++k) b.cp[k] = o.cp[k];
+        b.w1 = o.width / 2;                 // bezier.scm:63-65
+        b.w2 = b.w1 * b.w1;
+        b.eps8 = 8 * (o.width / 20);
+        return b;
+    };
+
+    // BVH over the world-level (chain -1) spheres, moving spheres and curves
     std::vector<PrimRef> refs;
     for (size_t i = 0; i < f.leaves.size(); ++i) {
         const LeafTmp& L = f.leaves[i];
-        if (L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE)) continue;
+        if (L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE && L.type != LEAF_BEZIER)) continue;
         const Obj& o = s->objs[L.obj];
         PrimRef r{};
         r.leaf = (int)i;
-        r.moving = L.type == LEAF_MSPHERE;
+        r.type = L.type;
         const double rad = std::fabs(o.r);
-        if (!r.moving) {
+        if (L.type == LEAF_SPHERE) {
             for (int k = 0; k < 3; ++k) { r.lo[k] = o.c0[k] - rad; r.hi[k] = o.c0[k] + rad; }
+        } else if (L.type == LEAF_BEZIER) {
+            const double w1 = std::fabs(o.width / 2);
+            for (int k = 0; k < 3; ++k) {
+                r.lo[k] = std::min(std::min(o.cp[k], o.cp[3 + k]), std::min(o.cp[6 + k], o.cp[9 + k])) - w1;
+                r.hi[k] = std::max(std::max(o.cp[k], o.cp[3 + k]), std::max(o.cp[6 + k], o.cp[9 + k])) + w1;
+            }
         } else {
             const double den = o.t1 - o.t0;
             const double ct0 = s->cam[22], ct1 = s->cam[23];
@@ -367,26 +384,27 @@ int commit_scene(Scene* s, int world) {
     std::vector<BvhLeaf> bleaf;
     int32_t bvh2_root = 0;
     int32_t lane_stack = 0;
+    bool bvh_has_bez = false;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         bb.build(0, (int)refs.size(), 0);
-        // leaf ranges: refs order -> sphere / moving-sphere array indices
-        std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0);
+        // leaf ranges: refs order -> sphere / moving-sphere / curve array indices
+        std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0), nb(refs.size() + 1, 0);
         for (size_t i = 0; i < refs.size(); ++i) {
-            ns[i + 1] = ns[i] + (refs[i].moving ? 0 : 1);
-            nm[i + 1] = nm[i] + (refs[i].moving ? 1 : 0);
+            ns[i + 1] = ns[i] + (refs[i].type == LEAF_SPHERE);
+            nm[i + 1] = nm[i] + (refs[i].type == LEAF_MSPHERE);
+            nb[i + 1] = nb[i] + (refs[i].type == LEAF_BEZIER);
         }
-        for (BvhNode& N : bb.nodes) {
-            if (N.c != -2) continue;
-            const int b = N.a, e = N.b;
-            N.a = ns[b]; N.b = ns[e] - ns[b]; N.c = nm[b]; N.d = nm[e] - nm[b];
-        }
+        bvh_has_bez = nb[refs.size()] > 0;
         bvh_nodes = std::move(bb.nodes);
         // per-lane layout: child boxes in the parent
         std::vector<int> inner_idx(bvh_nodes.size(), -1), leaf_idx(bvh_nodes.size(), -1);
         for (size_t i = 0; i < bvh_nodes.size(); ++i) {
-            if (bvh_nodes[i].c < 0) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); }
-            else { leaf_idx[i] = (int)bleaf.size(); bleaf.push_back({bvh_nodes[i].a, bvh_nodes[i].b, bvh_nodes[i].c, bvh_nodes[i].d}); }
+            const BvhNode& N = bvh_nodes[i];
+            if (N.c == -1) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); continue; }
+            leaf_idx[i] = (int)bleaf.size();
+            const int b = N.a, e = N.b;
+            bleaf.push_back({ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0});
         }
         auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
         for (size_t i = 0; i < bvh_nodes.size(); ++i) {
@@ -403,7 +421,7 @@ int commit_scene(Scene* s, int world) {
         // stack entries a per-lane traversal can need = depth of the BVH2
         std::vector<int> depth(bvh_nodes.size(), 0);
         for (size_t i = 0; i < bvh_nodes.size(); ++i)
-            if (bvh_nodes[i].c < 0) { depth[bvh_nodes[i].a] = depth[i] + 1; depth[bvh_nodes[i].b] = depth[i] + 1; }
+            if (bvh_nodes[i].c == -1) { depth[bvh_nodes[i].a] = depth[i] + 1; depth[bvh_nodes[i].b] = depth[i] + 1; }
         for (int dd : depth) lane_stack = std::max(lane_stack, dd);
         const int gid = (int)groups.size();
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
@@ -412,12 +430,13 @@ int commit_scene(Scene* s, int world) {
             const Obj& o = s->objs[L.obj];
             LeafInfo li{};
             li.type = L.type; li.group = gid; li.mat = o.mat; li.flip = L.flip;
-            li.inv_r = 1.0 / o.r; li.radius = o.r;
-            if (!r.moving) {
+            if (r.type == LEAF_SPHERE) {
+                li.inv_r = 1.0 / o.r; li.radius = o.r;
                 li.local = (int)sph.size();
                 sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
                 lsph.push_back(li);
-            } else {
+            } else if (r.type == LEAF_MSPHERE) {
+                li.inv_r = 1.0 / o.r; li.radius = o.r;
                 li.local = (int)msph.size();
                 MSphereRec m{};
                 m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
@@ -425,14 +444,22 @@ int commit_scene(Scene* s, int world) {
                 m.t0 = o.t0; m.den = o.t1 - o.t0;
                 msph.push_back(m);
                 lmsph.push_back(li);
+            } else {
+                li.local = (int)bez.size();
+                bez.push_back(bezier_rec(o));
+                lbez.push_back(li);
             }
         }
     }
     for (int ch : chain_order) {
-        for (int type = LEAF_SPHERE; type <= LEAF_RECT_YZ; ++type) {
-            if (use_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE)) continue;
+        for (int type = LEAF_SPHERE; type <= LEAF_BEZIER; ++type) {
+            if (use_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE || type == LEAF_BEZIER)) continue;
             Group g{type, ch, 0, 0};
-            size_t before = (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size() : rect.size();
+            auto type_size = [&]() {
+                return (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size()
+                     : (type == LEAF_BEZIER) ? bez.size() : rect.size();
+            };
+            size_t before = type_size();
             g.begin = (int)before;
             for (const LeafTmp& L : f.leaves) {
                 if (L.chain != ch || L.type != type) continue;
@@ -453,6 +480,10 @@ int commit_scene(Scene* s, int world) {
                     msph.push_back(m);
                     li.inv_r = 1.0 / o.r; li.radius = o.r;
                     lmsph.push_back(li);
+                } else if (type == LEAF_BEZIER) {
+                    li.local = (int)bez.size();
+                    bez.push_back(bezier_rec(o));
+                    lbez.push_back(li);
                 } else {
                     li.local = (int)rect.size();
                     RectRec r{};
@@ -461,14 +492,14 @@ int commit_scene(Scene* s, int world) {
                     lrect[type - LEAF_RECT_XY].push_back(li);
                 }
             }
-            size_t after = (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size() : rect.size();
+            size_t after = type_size();
             g.end = (int)after;
             if (after > before) groups.push_back(g);
         }
     }
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
     std::vector<LeafInfo> leaves;
-    int32_t base[5];
+    int32_t base[kLeafTypes];
     base[LEAF_SPHERE] = 0;
     for (auto& li : lsph) leaves.push_back(li);
     base[LEAF_MSPHERE] = (int32_t)leaves.size();
@@ -479,6 +510,8 @@ int commit_scene(Scene* s, int world) {
     for (int a = 0; a < 3; ++a) for (auto& li : lrect[a]) rl[li.local] = li;
     for (auto& li : rl) leaves.push_back(li);
     base[LEAF_RECT_XY] = base[LEAF_RECT_XZ] = base[LEAF_RECT_YZ] = rect_base;
+    base[LEAF_BEZIER] = (int32_t)leaves.size();
+    for (auto& li : lbez) leaves.push_back(li);
 
     std::vector<Chain> chains;
     for (auto& cv : f.chains) {
@@ -493,13 +526,13 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_msph, msph, &d.msph)) return rc;
     if (int rc = upload(s->d_rect, rect, &d.rect)) return rc;
     if (int rc = upload(s->d_groups, groups, &d.groups)) return rc;
-    if (int rc = upload(s->d_bvh, bvh_nodes, &d.bvh)) return rc;
-    d.n_bvh = (int)bvh_nodes.size();
+    if (int rc = upload(s->d_bez, bez, &d.bez)) return rc;
+    d.n_bez = (int)bez.size();
+    d.bvh_has_bez = bvh_has_bez ? 1 : 0;
     if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
     d.n_bvh2 = (int)bvh2.size();
     d.bvh2_root = bvh2_root;
-    d.traversal = traversal_mode();
     d.lane_stack = lane_stack;
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
@@ -509,7 +542,7 @@ int commit_scene(Scene* s, int world) {
     d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();
     d.n_groups = (int)groups.size(); d.n_chains = (int)chains.size(); d.n_leaves = (int)leaves.size();
     d.n_mats = (int)s->mats.size(); d.n_texs = (int)s->texs.size();
-    for (int k = 0; k < 5; ++k) d.leaf_base[k] = base[k];
+    for (int k = 0; k < kLeafTypes; ++k) d.leaf_base[k] = base[k];
     d.has_perlin = s->have_perlin ? 1 : 0;
     if (s->have_perlin) {
         if (int rc = upload(s->d_ranvec, s->ranvec, &d.ranvec)) return rc;
@@ -845,6 +878,33 @@ int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1,
     Obj o; o.type = O_RECT; o.axis = axis; o.mat = mat;
     o.a0 = a0; o.a1 = a1; o.b0 = b0; o.b1 = b1; o.k = k;
     return push_obj(s, std::move(o), out);
+}
+int rt_add_bezier(int scene, const double a[3], const double b[3], const double c[3], const double d[3],
+                  double width, int mat, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (!a || !b || !c || !d) return fail("rt_add_bezier: null control point");
+    if (check_mat(s, mat)) return 1;
+    if (!(width > 0.0) || !std::isfinite(width)) return fail("rt_add_bezier: width must be positive and finite");
+    Obj o; o.type = O_BEZIER; o.mat = mat; o.width = width;
+    const double* p[4] = {a, b, c, d};
+    for (int i = 0; i < 4; ++i) for (int k = 0; k < 3; ++k) o.cp[3 * i + k] = p[i][k];
+    return push_obj(s, std::move(o), out);
+}
+int rt_add_bezier_array(int scene, const double* cps, int n, double width, int mat, int* out_first) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out_first);
+    if (n < 0 || (n > 0 && !cps)) return fail("rt_add_bezier_array: invalid curve array");
+    if (check_mat(s, mat)) return 1;
+    if (!(width > 0.0) || !std::isfinite(width)) return fail("rt_add_bezier_array: width must be positive and finite");
+    *out_first = (int)s->objs.size();
+    s->objs.reserve(s->objs.size() + (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        Obj o; o.type = O_BEZIER; o.mat = mat; o.width = width;
+        for (int k = 0; k < 12; ++k) o.cp[k] = cps[(size_t)i * 12 + k];
+        s->objs.push_back(std::move(o));
+    }
+    return 0;
 }
 int rt_add_flip_normals(int scene, int child, int* out) {
     SCENE_OR_FAIL(s, scene);

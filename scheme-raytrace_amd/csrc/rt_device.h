@@ -22,8 +22,9 @@ constexpr int kMaxChain = 4;                   // instance ops per leaf chain
 enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum LeafType : int32_t { LEAF_SPHERE = 0, LEAF_MSPHERE = 1, LEAF_RECT_XY = 2, LEAF_RECT_XZ = 3,
-                          LEAF_RECT_YZ = 4 };
-constexpr int32_t GROUP_BVH = 5;               // group type: BVH over world-level spheres
+                          LEAF_RECT_YZ = 4, LEAF_BEZIER = 5 };
+constexpr int kLeafTypes = 6;
+constexpr int32_t GROUP_BVH = 6;               // group type: BVH over world-level spheres / curves
 enum ChainOp : int32_t { OP_TRANSLATE = 0, OP_ROTATE_Y = 1 };
 
 struct DevTexture {            // texture.scm:12-34
@@ -43,23 +44,21 @@ struct alignas(64) MSphereRec {                                        // center
     double den, pad0, pad1, pad2;
 };
 struct alignas(64) RectRec { double a0, a1, b0, b1, k, pad0, pad1, pad2; };
+// Cubic Bezier curve of a given width (bezier.scm:61-66): control points,
+// width1 = width/2, width2 = width1^2, eps8 = 8*(width/20).
+struct alignas(64) BezierRec { double cp[12]; double w1, w2, eps8, pad; };
+constexpr int kBezMaxDepth = 24;               // subdivision levels the curve test supports
 
-// BVH node over the world-level spheres and moving spheres (64 B = one
-// s_load_dwordx16).  Boxes are padded outward so culling is conservative: the
-// primitive tests are the exact f64 ones, the BVH only skips primitives that
-// cannot report a hit.  inner: c = -1, a/b = children, d = split axis;
-// leaf: spheres [a, a+b), moving spheres [c, c+d).
-struct alignas(64) BvhNode { double lo[3], hi[3]; int32_t a, b, c, d; };
-constexpr int kBvhStack = 64;                  // per-wave traversal stack (LDS)
-
-// Per-lane traversal layout (Aila & Laine style BVH2): both child boxes live
-// in the parent so one visit tests two boxes.  Child refs: >= 0 inner node,
-// < 0 leaf ~index into BvhLeaf.
+// BVH over the world-level spheres, moving spheres and curves, per-lane
+// traversal layout (Aila & Laine style BVH2): both child boxes live in the
+// parent so one visit tests two boxes.  Boxes are padded outward so culling is
+// conservative: the primitive tests are the exact f64 ones, the BVH only skips
+// primitives that cannot report a hit.  Child refs: >= 0 inner node, < 0 leaf
+// ~index into BvhLeaf.
 struct alignas(16) BvhNode2 { double lbox[6]; double rbox[6]; int32_t l, r, pad0, pad1; };
-struct BvhLeaf { int32_t sb, sn, mb, mn; };       // spheres [sb,sb+sn), moving [mb,mb+mn)
+struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
 constexpr int kLaneStack = 32;                 // per-lane traversal stack (LDS, stride = block size)
 constexpr int kLaneStackSmall = 12;            // kernel variant for BVHs at most 12 levels deep
-enum Traversal : int32_t { TRAV_WAVE = 0, TRAV_LANE = 1 };
 
 // Shade-side per-leaf record (indexed by leaf id).
 struct LeafInfo {
@@ -85,15 +84,15 @@ struct DevScene {
     const SphereRec* sph;  int32_t n_sph;
     const MSphereRec* msph; int32_t n_msph;
     const RectRec* rect;   int32_t n_rect;
+    const BezierRec* bez;  int32_t n_bez;
     const Group* groups;   int32_t n_groups;
-    const BvhNode* bvh;    int32_t n_bvh;
     const BvhNode2* bvh2;  int32_t n_bvh2;
     const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)
-    int32_t traversal;                             // Traversal
+    int32_t bvh_has_bez;                           // curves in the BVH: widen the box t range (see bvh_closest)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
-    int32_t leaf_base[5];                      // first leaf id of each LeafType
+    int32_t leaf_base[kLeafTypes];             // first leaf id of each LeafType
     const DevMaterial* mats; int32_t n_mats;
     const DevTexture* texs;  int32_t n_texs;
     const double* ranvec;                      // 256*3 (Perlin)

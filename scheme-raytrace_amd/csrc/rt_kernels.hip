@@ -166,59 +166,148 @@ __device__ __forceinline__ void sphere_test(const v3 o, const v3 d, const double
     }
 }
 
-// Conservative slab test of a padded BVH box against [0, closest].
-__device__ __forceinline__ bool box_hit(const BvhNode& N, const v3 o, const v3 inv, const double closest) {
-    const double tx0 = (N.lo[0] - o.x) * inv.x, tx1 = (N.hi[0] - o.x) * inv.x;
-    const double ty0 = (N.lo[1] - o.y) * inv.y, ty1 = (N.hi[1] - o.y) * inv.y;
-    const double tz0 = (N.lo[2] - o.z) * inv.z, tz1 = (N.hi[2] - o.z) * inv.z;
-    const double tnear = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
-    const double tfar = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), closest * 1.000000001));
-    return tnear <= tfar;
-}
 
-// Wave-uniform BVH traversal: the wave enters a node if ANY of its active
-// lanes' rays hits the node's box, so node records stay on the scalar path and
-// control flow stays uniform; each lane still keeps its own closest hit, and a
-// leaf's spheres get the same exact test as the brute-force loop.
-__device__ __forceinline__ void bvh_closest(const DevScene& sc, const v3 o, const v3 d, const double time,
-                                            double& closest, int32_t& best, uint32_t* stk) {
-    const double a = dot(d, d);
-    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
-    double last_t0 = 0.0, last_den = 0.0, frac = 0.0;
-    bool have = false;
+// ------------------------------------------------------------- curves
+// Cubic Bezier curve test (bezier.scm:13-214).  The ray is moved to a frame
+// where it starts at the origin and runs along +z (get-projection-mat); the
+// curve is subdivided at 0.5 down to a depth estimated from its flatness and
+// each surviving leaf segment is intersected in the xy plane.  The reference's
+// `converge` gives both children of a split the t it was called with, so the
+// curve's answer is min z over all leaf hits with z <= t; the recursion
+// becomes an explicit per-lane stack (private memory).
+struct BezRay { double m[12]; };        // rows 0..3, columns 0..2 of the 4x4 projection matrix
+
+__device__ __forceinline__ void bez_ray(const v3 o, const v3 d, BezRay& R) {
+    const double ox = -o.x, oy = -(-o.z), oz = -o.y;
+    const v3 rd = unit(d);
+    const double lx = rd.x, ly = -rd.z, lz = rd.y;
+    const double dd = sqrt(lx * lx + lz * lz);
+    double r[9];
+    if (dd == 0.0) {
+        const double ang = (ly >= 0.0) ? -(kPi / 2) : (kPi / 2);
+        const double cs = cos(ang), sn = sin(ang);
+        r[0] = 1.0; r[1] = 0.0; r[2] = 0.0;
+        r[3] = 0.0; r[4] = cs;  r[5] = -sn;
+        r[6] = 0.0; r[7] = sn;  r[8] = cs;
+    } else {
+        r[0] = lz / dd;   r[1] = (-1.0 * lx * ly) / dd; r[2] = lx;
+        r[3] = 0.0;       r[4] = dd;                    r[5] = ly;
+        r[6] = (-lx) / dd; r[7] = (-1.0 * ly * lz) / dd; r[8] = lz;
+    }
+    // array-mul with the translation: rows 0..2 are the rotation, row 3 = o' R
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R.m[k] = r[k];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R.m[9 + j] = ((ox * r[j] + oy * r[3 + j]) + oz * r[6 + j]) + 0.0;
+}
+// transform (bezier.scm:49-55): row vector (x, -z, y, 1) times the matrix
+__device__ __forceinline__ v3 bez_xf(const BezRay& R, const double x, const double y, const double z) {
+    const double a = x, b = -z, c = y;
+    return mk(((a * R.m[0] + b * R.m[3]) + c * R.m[6]) + R.m[9],
+              ((a * R.m[1] + b * R.m[4]) + c * R.m[7]) + R.m[10],
+              ((a * R.m[2] + b * R.m[5]) + c * R.m[8]) + R.m[11]);
+}
+struct Bez4 { v3 p0, p1, p2, p3; };
+__device__ __forceinline__ v3 bez_point(const Bez4& c, const double t) {       // bez-p :67-77
+    const double t2 = t * t, t3 = t2 * t;
+    const double u = 1.0 - t, u2 = u * u, u3 = u2 * u;
+    return ((c.p0 * u3 + c.p1 * (3.0 * u2 * t)) + c.p2 * (3.0 * u * t2)) + c.p3 * t3;
+}
+__device__ __forceinline__ v3 half_div(const v3 a, const v3 b) { return a * 0.5 + b * 0.5; }   // :45-47, t = 0.5
+__device__ __forceinline__ void bez_split(const Bez4& c, Bez4& l, Bez4& r) {    // split :78-87
+    const v3 sp = bez_point(c, 0.5);
+    const v3 nbc = half_div(c.p1, c.p2);
+    const v3 lb = half_div(c.p0, c.p1);
+    const v3 lc = half_div(lb, nbc);
+    const v3 rc = half_div(c.p2, c.p3);
+    const v3 rb = half_div(nbc, rc);
+    l.p0 = c.p0; l.p1 = lb; l.p2 = lc; l.p3 = sp;
+    r.p0 = sp; r.p1 = rb; r.p2 = rc; r.p3 = c.p3;
+}
+__device__ __forceinline__ v3 bez_tan(const Bez4& c, const bool one) {         // bez-tan-vec :106-117
+    const v3 ca = ((c.p1 * 3.0 + c.p3) + c.p2 * -3.0) + c.p0 * -1.0;
+    const v3 cb = ((c.p0 + c.p1 * -2.0) + c.p2) * 3.0;
+    const v3 cc = (c.p1 - c.p0) * 3.0;
+    const double k2 = one ? 3.0 : 0.0, k1 = one ? 2.0 : 0.0;
+    return unit((ca * k2 + cb * k1) + cc);
+}
+__device__ __forceinline__ double dot2d(const v3 a, const v3 b) { return (a.x * b.x + a.y * b.y) + 0.0 * 0.0; }
+
+struct BezFrame { Bez4 c; double v0; int depth; };
+
+// Returns true and the curve's t if it reports a hit for t-max `tmax`.
+__device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
+    const double w1 = B.w1, w2 = B.w2;
+    Bez4 c;
+    c.p0 = bez_xf(R, B.cp[0], B.cp[1], B.cp[2]);
+    c.p1 = bez_xf(R, B.cp[3], B.cp[4], B.cp[5]);
+    c.p2 = bez_xf(R, B.cp[6], B.cp[7], B.cp[8]);
+    c.p3 = bez_xf(R, B.cp[9], B.cp[10], B.cp[11]);
+    // flatness -> subdivision depth (:180-193)
+    double l0 = -kTmax;
+    {
+        const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
+        l0 = fmax(fmax(x0, y0), l0);
+        const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
+        l0 = fmax(fmax(x1, y1), l0);
+    }
+    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / B.eps8) / log(4.0);
+    int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
+    if (maxd > kBezMaxDepth) maxd = kBezMaxDepth;   // beyond any width / extent ratio a scene uses
+    bool found = false;
+    double best = tmax;
+    BezFrame stk[kBezMaxDepth + 1];
     int sp = 0;
-    uint32_t node = 0;
+    double v0 = 0.0;
+    int depth = maxd;
     for (;;) {
-        const BvhNode N = sc.bvh[node];
-        const bool h = box_hit(N, o, inv, closest);
-        if (__ballot(h)) {
-            if (N.c < 0) {                                    // inner: near child first
-                const double dax = (N.d == 0) ? d.x : (N.d == 1) ? d.y : d.z;
-                const int neg = __builtin_amdgcn_readfirstlane((int)(dax < 0.0));
-                const uint32_t near = neg ? (uint32_t)N.b : (uint32_t)N.a;
-                const uint32_t far = neg ? (uint32_t)N.a : (uint32_t)N.b;
-                if (sp < kBvhStack) stk[sp++] = far;
-                node = near;
+        // bounding-box cull (:123-128)
+        const double zmn = fmin(fmin(c.p0.z, c.p1.z), fmin(c.p2.z, c.p3.z)) - w1;
+        const double zmx = fmax(fmax(c.p0.z, c.p1.z), fmax(c.p2.z, c.p3.z)) + w1;
+        const double xmn = fmin(fmin(c.p0.x, c.p1.x), fmin(c.p2.x, c.p3.x)) - w1;
+        const double xmx = fmax(fmax(c.p0.x, c.p1.x), fmax(c.p2.x, c.p3.x)) + w1;
+        const double ymn = fmin(fmin(c.p0.y, c.p1.y), fmin(c.p2.y, c.p3.y)) - w1;
+        const double ymx = fmax(fmax(c.p0.y, c.p1.y), fmax(c.p2.y, c.p3.y)) + w1;
+        const bool culled = zmn >= tmax || zmx <= 0.000001 || xmn >= w1 || xmx <= -w1 || ymn >= w1 || ymx <= -w1;
+        if (!culled) {
+            const double span = ldexp(1.0, depth - maxd);       // vn - v0 at this level
+            if (depth >= 0) {                                   // split, left first (:167-175)
+                Bez4 l, r;
+                bez_split(c, l, r);
+                stk[sp].c = r; stk[sp].v0 = v0 + span * 0.5; stk[sp].depth = depth - 1; ++sp;
+                c = l; depth -= 1;
                 continue;
             }
-            for (int s = N.a; s < N.a + N.b; ++s) {
-                const SphereRec S = sc.sph[s];
-                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
-            }
-            for (int s = N.c; s < N.c + N.d; ++s) {
-                const MSphereRec S = sc.msph[s];
-                if (!have || S.t0 != last_t0 || S.den != last_den) {   // uniform branch
-                    frac = (time - S.t0) / S.den;
-                    last_t0 = S.t0; last_den = S.den; have = true;
+            // leaf segment (:130-166)
+            const double vn = v0 + span;
+            const v3 dir = c.p3 - c.p0;
+            v3 dp0 = bez_tan(c, false);
+            if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
+            if (!(dot2d(dp0, c.p0 * -1.0) < 0.0)) {
+                v3 dpn = bez_tan(c, true);
+                if (dot2d(dir, dpn) < 0.0) dpn = dpn * -1.0;
+                if (!(dot2d(dpn, c.p3) < 0.0)) {
+                    double w = dir.x * dir.x + dir.y * dir.y;
+                    if (w != 0.0) {
+                        w = (c.p0.x * dir.x + c.p0.y * dir.y) / (-w);
+                        w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
+                        const double v = v0 * (1.0 - w) + vn * w;
+                        const v3 p = bez_point(c, v);             // sub-curve at the global v (Q11)
+                        if (!(p.x * p.x + p.y * p.y >= w2 || p.z <= 0.0001 || tmax < p.z)) {
+                            if (!found || p.z < best) best = p.z;
+                            found = true;
+                        }
+                    }
                 }
-                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
             }
         }
         if (sp == 0) break;
-        node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+        --sp;
+        c = stk[sp].c; v0 = stk[sp].v0; depth = stk[sp].depth;
     }
+    if (!(found && kTmin < best)) return false;                 // :201
+    tout = best;
+    return true;
 }
 
 // Per-lane BVH traversal: every lane walks its own path through the BVH2
@@ -234,11 +323,20 @@ __device__ __forceinline__ bool box_hit_t(const double* bx, const v3 o, const v3
     return tnear <= tfar;
 }
 
+template <bool BEZ>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
     const double a = dot(d, d);
     const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
+    // A curve reports t as a distance along unit(d) (Q10), i.e. raw ray
+    // parameter t/|d|: for |d| < 1 the box range must reach closest/|d|.
+    double tscale = 1.0;
+    BezRay R;
+    if (BEZ && sc.bvh_has_bez) {
+        tscale = fmax(1.0, 1.0 / sqrt(a));
+        bez_ray(o, d, R);
+    }
     const uint32_t stride = blockDim.x;
     int sp = 0;
     int32_t node = sc.bvh2_root;
@@ -246,8 +344,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
         if (node >= 0) {
             const BvhNode2 N = sc.bvh2[node];
             double tl, tr;
-            const bool hl = box_hit_t(N.lbox, o, inv, closest, tl);
-            const bool hr = box_hit_t(N.rbox, o, inv, closest, tr);
+            const bool hl = box_hit_t(N.lbox, o, inv, closest * tscale, tl);
+            const bool hr = box_hit_t(N.rbox, o, inv, closest * tscale, tr);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
                 if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
@@ -268,6 +366,12 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
             }
+            if (BEZ) {
+                for (int s = L.bb; s < L.bb + L.bn; ++s) {
+                    double t;
+                    if (bezier_test(sc.bez[s], R, closest, t)) { closest = t; best = sc.leaf_base[LEAF_BEZIER] + s; }
+                }
+            }
         }
         if (sp == 0) break;
         --sp;
@@ -280,16 +384,16 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 // (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
 // walks the same group / primitive sequence, so the primitive records are
 // fetched once per wave through the scalar unit.
+template <bool BEZ>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
-                                               const double time, double& closest, uint32_t* stk,
-                                               uint32_t* lstk, const int lmax) {
+                                               const double time, double& closest, uint32_t* lstk,
+                                               const int lmax) {
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
         const Group G = sc.groups[g];
         if (G.type == GROUP_BVH) {
-            if (sc.traversal == TRAV_LANE) bvh_closest_lane(sc, o0, d0, time, closest, best, lstk, lmax);
-            else bvh_closest(sc, o0, d0, time, closest, best, stk);
+            bvh_closest_lane<BEZ>(sc, o0, d0, time, closest, best, lstk, lmax);
             continue;
         }
         v3 o = o0, d = d0;
@@ -313,6 +417,15 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
                 }
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
+            }
+        } else if (G.type == LEAF_BEZIER) {                // bezier.scm:176-214
+            if (BEZ) {
+                BezRay R;
+                bez_ray(o, d, R);
+                for (int s = G.begin; s < G.end; ++s) {
+                    double t;
+                    if (bezier_test(sc.bez[s], R, closest, t)) { closest = t; best = base + s; }
+                }
             }
         } else {                                            // geometry.scm:376-431
             // XY: k on z, (a,b) = (x,y); XZ: k on y, (x,z); YZ: k on x, (y,z)
@@ -428,12 +541,11 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
 // the spot (sky); hits are appended to the queue of their material type so
 // each shade kernel runs one material's code (wavefront material queues).
 // =====================================================================
-template <int LS>
+template <int LS, bool BEZ>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                 uint32_t* __restrict__ queues, uint32_t qstride,
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t s_stack[4 * kBvhStack];
     __shared__ uint32_t s_lstack[256 * LS];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
@@ -444,8 +556,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
         const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
         double t;
-        const int32_t leaf = closest_hit(sc, o, d, st.tm[i], t, s_stack + (threadIdx.x >> 6) * kBvhStack,
-                                         s_lstack + threadIdx.x, LS);
+        const int32_t leaf = closest_hit<BEZ>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS);
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             const uint32_t wid = st.wid[i];
@@ -551,8 +662,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         nrm = mk(0.0, 0.0, 1.0);
     } else if (li.type == LEAF_RECT_XZ) {
         nrm = mk(0.0, 1.0, 0.0);
-    } else {
+    } else if (li.type == LEAF_RECT_YZ) {
         nrm = mk(1.0, 0.0, 0.0);
+    } else {
+        nrm = d * -1.0;                                      // curve: (v:scale (dir r) -1), bezier.scm:204
     }
     if (li.flip) nrm = nrm * -1.0;                          // flip-normals :438
     if (G.chain >= 0) chain_hit(sc.chains[G.chain], pt, nrm);
@@ -680,12 +793,11 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
-template <int LS>
+template <int LS, bool BEZ>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ seg_count) {
     __shared__ PerlinLds P;
-    __shared__ uint32_t s_stack[4 * kBvhStack];
     __shared__ uint32_t s_lstack[256 * LS];
     stage_perlin(sc, P);
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
@@ -697,8 +809,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
         for (;;) {
             double t;
             ++segs;
-            const int32_t leaf = closest_hit(sc, p.o, p.d, p.time, t, s_stack + (threadIdx.x >> 6) * kBvhStack,
-                                             s_lstack + threadIdx.x, LS);
+            const int32_t leaf = closest_hit<BEZ>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS);
             if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
             if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
         }
@@ -747,12 +858,13 @@ hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathS
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
                          uint32_t* counts, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    if (sc.lane_stack <= kLaneStackSmall)
-        hipLaunchKernelGGL(k_extend<kLaneStackSmall>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,
-                           qstride, shard_cap, counts);
-    else
-        hipLaunchKernelGGL(k_extend<kLaneStack>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,
-                           qstride, shard_cap, counts);
+#define RT_EXTEND(LS, BEZ)                                                                                   \
+    hipLaunchKernelGGL((k_extend<LS, BEZ>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,   \
+                       qstride, shard_cap, counts)
+    const bool small = sc.lane_stack <= kLaneStackSmall;
+    if (sc.n_bez > 0) { if (small) RT_EXTEND(kLaneStackSmall, true); else RT_EXTEND(kLaneStack, true); }
+    else { if (small) RT_EXTEND(kLaneStackSmall, false); else RT_EXTEND(kLaneStack, false); }
+#undef RT_EXTEND
     return hipGetLastError();
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
@@ -781,10 +893,12 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, unsigned long long* seg_count, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-    if (sc.lane_stack <= kLaneStackSmall)
-        hipLaunchKernelGGL(k_finish<kLaneStackSmall>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
-    else
-        hipLaunchKernelGGL(k_finish<kLaneStack>, dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count);
+#define RT_FINISH(LS, BEZ) \
+    hipLaunchKernelGGL((k_finish<LS, BEZ>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count)
+    const bool small = sc.lane_stack <= kLaneStackSmall;
+    if (sc.n_bez > 0) { if (small) RT_FINISH(kLaneStackSmall, true); else RT_FINISH(kLaneStack, true); }
+    else { if (small) RT_FINISH(kLaneStackSmall, false); else RT_FINISH(kLaneStack, false); }
+#undef RT_FINISH
     return hipGetLastError();
 }
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {

@@ -59,6 +59,9 @@ _SIGNATURES = {
                              ctypes.c_double, ctypes.c_int, _c_int_p],
     "rt_add_rect": [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                     ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_int_p],
+    "rt_add_bezier": [ctypes.c_int, _c_double_p, _c_double_p, _c_double_p, _c_double_p, ctypes.c_double,
+                      ctypes.c_int, _c_int_p],
+    "rt_add_bezier_array": [ctypes.c_int, _c_double_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_int_p],
     "rt_add_flip_normals": [ctypes.c_int, ctypes.c_int, _c_int_p],
     "rt_add_box": [ctypes.c_int, _c_double_p, _c_double_p, ctypes.c_int, _c_int_p],
     "rt_add_translate": [ctypes.c_int, ctypes.c_int, _c_double_p, _c_int_p],

@@ -90,6 +90,15 @@ class GpuBuilder:
     def rect(self, axis, a0, a1, b0, b1, k, mat):
         return self._out("rt_add_rect", axis, a0, a1, b0, b1, k, mat)
 
+    def bezier(self, a, b, c, d, width, mat):
+        return self._out("rt_add_bezier", dvec(a), dvec(b), dvec(c), dvec(d), width, mat)
+
+    def bezier_array(self, cps, width, mat):
+        """cps: contiguous float64 array of shape (n, 12); returns the first id."""
+        cps = np.ascontiguousarray(cps, dtype=np.float64)
+        ptr = cps.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        return self._out("rt_add_bezier_array", ptr, int(cps.shape[0]), width, mat)
+
     def flip_normals(self, obj):
         return self._out("rt_add_flip_normals", obj)
 

@@ -128,6 +128,30 @@ def make_yz_rect(y0, y1, z0, z1, k, material):
     return Hitable("rect", 2, float(y0), float(y1), float(z0), float(z1), float(k), material)
 
 
+def make_bezier(a, b, c, d, width, material):
+    """b:make-bezier (bezier.scm:61-223): cubic Bezier curve a..d of the given
+    width.  Its hit t is a distance along unit(dir) used as a parameter of the
+    raw ray (Q10) and its normal is -dir (Q12); see DESIGN.md."""
+    _need(material, Material, "make-bezier material")
+    if not float(width) > 0.0:
+        raise ValueError("make-bezier: width must be positive")
+    return Hitable("bezier", v.vec3(*a), v.vec3(*b), v.vec3(*c), v.vec3(*d), float(width), material)
+
+
+def bezier_array(cps, width, material):
+    """bezier->objs (points.scm:45-53) in bulk: ``cps`` is an (n, 12) float64
+    array of control points (a, b, c, d per row), one curve per row, all of
+    one width and material.  Behaves as the list of those curves."""
+    import numpy as np
+    _need(material, Material, "bezier->objs material")
+    if not float(width) > 0.0:
+        raise ValueError("bezier->objs: width must be positive")
+    arr = np.ascontiguousarray(cps, dtype=np.float64)
+    if arr.ndim != 2 or arr.shape[1] != 12:
+        raise ValueError("bezier->objs: control points must have shape (n, 12)")
+    return Hitable("curves", arr, float(width), material)
+
+
 def flip_normals(obj):
     """g:flip-normals (geometry.scm:433-442)."""
     _need(obj, Hitable, "flip-normals")
@@ -285,6 +309,11 @@ def emit(scene, b):
             r = b.moving_sphere(a[0], a[1], a[2], a[3], a[4], mat(a[5]))
         elif o.kind == "rect":
             r = b.rect(a[0], a[1], a[2], a[3], a[4], a[5], mat(a[6]))
+        elif o.kind == "bezier":
+            r = b.bezier(a[0], a[1], a[2], a[3], a[4], mat(a[5]))
+        elif o.kind == "curves":
+            first = b.bezier_array(a[0], a[1], mat(a[2]))
+            r = b.list(list(range(first, first + a[0].shape[0])))
         elif o.kind == "flip":
             r = b.flip_normals(obj(a[0]))
         elif o.kind == "box":

@@ -152,6 +152,96 @@ def test_scene_bvh_sah(nx, ny, seed=SCENE_SEED):
     return g.make_scene([ground, g.make_bvh_with_sah(spheres, 0, 0)], camera_for(nx, ny), g.sky_color)
 
 
+def test_bezier(nx, ny):
+    """test-bezier (main.scm:237-277): checker ground, six spheres and three
+    width-0.1 curves under one make-bvh-node; *camera*, sky-color."""
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    green = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.45, 0.15)))
+    blue = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.15, 0.45)))
+    ground = g.make_sphere(v.vec3(0, -100.5, -1), 100,
+                           g.make_lambertian(g.checker_texture(g.constant_texture(v.vec3(0.2, 0.3, 0.1)),
+                                                               g.constant_texture(v.vec3(0.9, 0.9, 0.9)))))
+    inner = [
+        g.make_sphere(v.vec3(2, 0, 2), 0.5, red),
+        g.make_sphere(v.vec3(-2, 0, -2), 0.5, green),
+        g.make_sphere(v.vec3(-1, 0, -1), 0.1, blue),
+        g.make_sphere(v.vec3(-0.8, 1, 1), 0.1, blue),
+        g.make_sphere(v.vec3(0.8, -1, 1), 0.1, blue),
+        g.make_sphere(v.vec3(1, 0, -1), 0.1, blue),
+        g.make_bezier(v.vec3(-1, 0, -1), v.vec3(-0.8, 1, 1), v.vec3(0.8, -1, 1), v.vec3(1, 0, -1), 0.1, red),
+        g.make_bezier(v.vec3(-1, 0, 1), v.vec3(-0.8, 1, -1), v.vec3(0.8, -1, -1), v.vec3(1, 0, 1), 0.1, red),
+        g.make_bezier(v.vec3(-1, 0, 2), v.vec3(-0.8, 1, -2), v.vec3(0.8, -1, -2), v.vec3(1, 0, 2), 0.1, red),
+    ]
+    return g.make_scene([ground, g.make_bvh_node(inner, 0, 0)], camera_for(nx, ny), g.sky_color)
+
+
+def cornell_bezier(nx, ny):
+    """cornell-bezier (main.scm:353-373): the Cornell frame with one width-10
+    red curve in place of the boxes."""
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    green = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.45, 0.15)))
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(3, 3, 3)))
+    objs = [
+        g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, green)),
+        g.make_yz_rect(0, 555, 0, 555, 0, red),
+        g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)),
+        g.flip_normals(g.make_xz_rect(0, 555, 0, 555, 555, white)),
+        g.make_xz_rect(0, 555, 0, 555, 0, white),
+        g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white)),
+        g.make_bezier(v.vec3(130, 0, 65), v.vec3(150, 0, 190), v.vec3(130, 0, 190), v.vec3(265, 0, 295), 10, red),
+    ]
+    return g.make_scene(objs, cornell_camera_for(nx, ny), g.sky_color)
+
+
+CURVE_SEED = 0x5EED0005
+
+
+def random_polyline_curves(n_curves, seed=CURVE_SEED, segs_per_line=256, lo=10.0, hi=545.0, step=6.0):
+    """Control points of ``n_curves`` curves: seeded random-walk polylines
+    inside the Cornell frame, each turned into ``segs_per_line`` segments by
+    the points->bezier rule (points.scm:22-43, vectorised with the same
+    operation order as rtamd.points).  Returns an (n, 12) float64 array."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    n_lines = max(1, -(-n_curves // segs_per_line))
+    npts = segs_per_line + 3
+    start = rng.uniform(lo + 70.0, hi - 70.0, size=(n_lines, 1, 3))
+    steps = rng.uniform(-step, step, size=(n_lines, npts - 1, 3))
+    pts = np.concatenate([start, start + np.cumsum(steps, axis=1)], axis=1)
+    pts = np.clip(pts, lo, hi)
+    pt, p1, p2, p3 = pts[:, :-3], pts[:, 1:-2], pts[:, 2:-1], pts[:, 3:]
+    d1 = (p2 - pt) * (1 / 6)
+    d2 = (p3 - p1) * (1 / 6)
+    cps = np.concatenate([p1, p1 + d1, p2 - d2, p2], axis=2).reshape(-1, 12)
+    return np.ascontiguousarray(cps[:n_curves])
+
+
+def cornell_curves(nx, ny, n_curves=1 << 20, width=0.5, seed=CURVE_SEED):
+    """Config C5: ~1M red lambertian curves (width 0.1 x scale 5) in a BVH
+    inside the cornell-bezier frame (main.scm:353-373), *cornell-camera*."""
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    green = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.45, 0.15)))
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(3, 3, 3)))
+    curves = g.bezier_array(random_polyline_curves(n_curves, seed), width, red)
+    objs = [
+        g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, green)),
+        g.make_yz_rect(0, 555, 0, 555, 0, red),
+        g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)),
+        g.flip_normals(g.make_xz_rect(0, 555, 0, 555, 555, white)),
+        g.make_xz_rect(0, 555, 0, 555, 0, white),
+        g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white)),
+        g.make_bvh_node([curves], 0, 0),
+    ]
+    return g.make_scene(objs, cornell_camera_for(nx, ny), g.sky_color)
+
+
+def cornell_curves_small(nx, ny):
+    """C5's generator at 4096 curves (oracle-checkable without a BVH)."""
+    return cornell_curves(nx, ny, n_curves=4096, width=3.0)
+
+
 SCENES = {
     "cover": random_scene,
     "cover_marble": marble_random_scene,
@@ -159,4 +249,8 @@ SCENES = {
     "test_scene2": test_scene2,
     "cornell": cornell_box,
     "bvh_sah": test_scene_bvh_sah,
+    "test_bezier": test_bezier,
+    "cornell_bezier": cornell_bezier,
+    "curves": cornell_curves,
+    "curves_small": cornell_curves_small,
 }

@@ -129,6 +129,32 @@ class Ref:
         return self.it.eval(lam, self.main)
 
 
+def _bezier_rays():
+    """Rays aimed at points of the two KAT curves (plus misses): from a camera
+    like *camera*, straight down z (the d == 0 branch of get-projection-mat,
+    bezier.scm:24-31), with short (|d| < 1) and long directions."""
+    def bez(cp, t):
+        u = 1 - t
+        return [cp[0][k] * u ** 3 + 3 * cp[1][k] * u * u * t + 3 * cp[2][k] * u * t * t + cp[3][k] * t ** 3
+                for k in range(3)]
+    c1 = [(-1, 0, -1), (-0.8, 1, 1), (0.8, -1, 1), (1, 0, -1)]
+    c2 = [(130, 0, 65), (150, 0, 190), (130, 0, 190), (265, 0, 295)]
+    out = []
+    for t in (0.05, 0.3, 0.5, 0.77, 0.95):
+        p = bez(c1, t)
+        for o, sc in (((0, 5, 5), 1.0), ((0.3, 2, 6), 0.5), ((-3, 0.5, 1), 2.0)):
+            d = [(p[k] - o[k]) * sc for k in range(3)]
+            out.append((o, tuple(d), 0.0))
+            out.append((o, (d[0] + 0.01, d[1], d[2] - 0.02), 0.0))
+        out.append(((p[0], p[1], 4.0), (0.0, 0.0, -1.0), 0.0))          # along -z
+        out.append(((p[0] + 0.03, p[1], -4.0), (0.0, 0.0, 1.0), 0.0))   # along +z, offset inside width
+        q = bez(c2, t)
+        out.append(((278, 278, -800), tuple(q[k] - (278, 278, -800)[k] for k in range(3)), 0.0))
+        out.append(((278, 400, 100), tuple(q[k] - (278, 400, 100)[k] for k in range(3)), 0.0))
+    out.append(((0, 5, 5), (0, 1, 0), 0.0))                              # miss
+    return out
+
+
 def kat(ref):
     it = ref.it
     out = {}
@@ -203,12 +229,17 @@ def kat(ref):
                          " (m:make-lambertian (t:constant-texture (v:vec3 0.73 0.73 0.73)))) 15) (v:vec3 265 0 295))"
                          " (g:flip-normals (g:make-xz-rect 213 343 227 332 554"
                          " (m:make-diffuse-light (t:constant-texture (v:vec3 3 3 3))))))",
+        "bezier": "(list (b:make-bezier (v:vec3 -1 0 -1) (v:vec3 -0.8 1 1) (v:vec3 0.8 -1 1) (v:vec3 1 0 -1)"
+                  " 0.1 (m:make-lambertian (t:constant-texture (v:vec3 0.65 0.05 0.05))))"
+                  " (b:make-bezier (v:vec3 130 0 65) (v:vec3 150 0 190) (v:vec3 130 0 190) (v:vec3 265 0 295)"
+                  " 10 (m:make-lambertian (t:constant-texture (v:vec3 0.73 0.73 0.73)))))",
     }
     rays = {
         "spheres": [((0, 0, 0), (0, 0, -1), 0.0), ((0, 0, 0), (-1, 0.1, -1), 0.0), ((0, 0, 0), (0.9, 0.05, -1), 0.7),
                     ((0, 0, 0), (0.9, 0.05, -1), 0.0), ((0, 1, 0), (0, -1, 0.001), 0.0), ((-1, 0, -1), (0, 0, 1), 0.0)],
         "cornell_boxes": [((200, 80, -500), (0, 0, 1), 0.0), ((278, 278, -800), (0.05, 0.3, 1), 0.0),
                           ((300, 100, 400), (0.1, -0.2, -1), 0.0), ((278, 500, 278), (0.01, 1, 0.02), 0.0)],
+        "bezier": _bezier_rays(),
     }
     hobj = it.modules["geometry"].lookup(ms.sym("hit-obj-list"))
     for name, src in setup.items():
@@ -224,6 +255,12 @@ def kat(ref):
                 res.append([H(o), H(d), H(tm), [H(rec[0]), H(rec[1]), H(rec[2])]])
         hits[name] = res
     out["hits"] = hits
+    # points.scm: polyline -> Catmull-Rom Bezier control points
+    pts_mod = it.modules["points"]
+    poly = [(0.0, 0.0, 0.0), (1.0, 2.0, 0.5), (2.5, 1.0, -1.0), (4.0, 3.0, 0.25), (3.0, 5.5, 2.0), (1.5, 4.0, 3.0)]
+    res = call(pts_mod, "points->bezier", [vec3(q) for q in poly])
+    out["points_to_bezier"] = {"points": H(poly), "beziers": [[H(list(c)) for c in ms.to_list(b)]
+                                                              for b in ms.to_list(res)]}
     return out
 
 
@@ -236,10 +273,14 @@ SCENE_EXPR = {
     # the reference's default *scene* (main.scm:437): 100 line-upped spheres
     # (random albedos, main.scm:177-194) under its own SAH BVH (geometry.scm:294-371)
     "bvh_sah": ("defines", ["*spheres-list*", "*bvh-sah-node*", "test-scene-bvh-sah"]),
+    # cubic Bezier curves (bezier.scm): three curves in a make-bvh-node, and the
+    # Cornell frame with one wide curve
+    "test_bezier": ("define", "test-bezier"),
+    "cornell_bezier": ("define", "cornell-bezier"),
 }
 
 SIZES = {"test_scene": (24, 16, 3), "test_scene2": (24, 16, 3), "cornell": (16, 16, 6), "cover": (24, 12, 2),
-         "bvh_sah": (24, 12, 2)}
+         "bvh_sah": (24, 12, 2), "test_bezier": (32, 18, 2), "cornell_bezier": (16, 16, 4)}
 
 
 def render(ref, name):

@@ -20,7 +20,7 @@ from rtamd import perlin, scenes
 from rtamd.camera import make_camera
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENES = ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah"]
+SCENES = ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier", "cornell_bezier"]
 
 
 def F(x):
@@ -191,3 +191,36 @@ def test_moving_sphere_time_semantics(kat):
     t07 = [r for r in rays if F(r[2]) == 0.7][0]
     t00 = [r for r in rays if F(r[2]) == 0.0 and r[1] == t07[1]][0]
     assert t07[3] is None and t00[3] is not None
+
+
+def test_bezier_hits(kat, oracle_mod):
+    """Closest hits against two curves (bezier.scm:176-214) through the
+    reference's hit-obj-list: t (a distance along unit(dir), Q10), the point
+    on the raw ray at that t and the normal -dir (Q12), bit for bit.  The
+    rays include the straight-down-z case (get-projection-mat's d = 0 branch)
+    and |dir| != 1."""
+    from rtamd import scene as g
+    lam = g.make_lambertian
+    ct = g.constant_texture
+    objs = [g.make_bezier((-1, 0, -1), (-0.8, 1, 1), (0.8, -1, 1), (1, 0, -1), 0.1, lam(ct((0.65, 0.05, 0.05)))),
+            g.make_bezier((130, 0, 65), (150, 0, 190), (130, 0, 190), (265, 0, 295), 10,
+                          lam(ct((0.73, 0.73, 0.73))))]
+    sc = g.make_scene(objs, make_camera((0, 0, 0), (0, 0, -1), (0, 1, 0), 90, 1, 0, 1, 0, 1), g.black)
+    o = oracle_mod.build_scene(sc)
+    rays = kat["hits"]["bezier"]
+    assert sum(r[3] is not None for r in rays) >= 40
+    for orig, d, tm, rec in rays:
+        got = o.hit_world(F(orig), F(d), F(tm))
+        if rec is None:
+            assert got is None
+        else:
+            assert got is not None
+            assert [got[0]] + list(got[1:4]) + list(got[4:7]) == [F(rec[0])] + F(rec[1]) + F(rec[2])
+
+
+def test_points_to_bezier(kat):
+    """points->bezier (points.scm:28-43): Catmull-Rom control points."""
+    from rtamd import points
+    k = kat["points_to_bezier"]
+    got = points.points_to_bezier([tuple(p) for p in F(k["points"])])
+    assert [[list(c) for c in b] for b in got] == [[F(c) for c in b] for b in k["beziers"]]

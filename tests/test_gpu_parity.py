@@ -44,6 +44,9 @@ def _both(scene, nx, ny, spp, oracle_mod, spp_begin=0, seed=SEED):
     ("test_scene2", 64, 48, 8),
     ("cornell", 48, 48, 16),
     ("bvh_sah", 64, 36, 4),
+    ("test_bezier", 64, 36, 4),
+    ("cornell_bezier", 48, 48, 8),
+    ("curves_small", 64, 36, 2),
 ])
 def test_scene_parity(name, nx, ny, spp, gpu_ctx, oracle_mod):
     scene = scenes.SCENES[name](nx, ny)
@@ -175,8 +178,8 @@ def test_device_resolve_matches_host(gpu_ctx):
 
 
 def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
-    """The wave-uniform BVH only culls: the image equals the brute-force flat
-    list (geometry.scm:33-50) bit for bit."""
+    """The BVH only culls: the image equals the brute-force flat list
+    (geometry.scm:33-50) bit for bit."""
     nx, ny, spp = 64, 40, 4
     monkeypatch.setenv("RTAMD_BVH_MIN", "1000000000")
     flat_scene = scenes.random_scene(nx, ny)
@@ -189,7 +192,8 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah"])
+@pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier",
+                                  "cornell_bezier"])
 def test_gpu_vs_reference_fixtures(name, gpu_ctx):
     """The GPU against the outputs of the REFERENCE's own source, executed
     (tests/golden/make_golden.py): same scene, seed and streams."""
@@ -207,3 +211,34 @@ def test_gpu_vs_reference_fixtures(name, gpu_ctx):
     assert nbad <= max(2, npx // 100)
     img = gpu.resolve_u8(acc, nx, ny, spp)
     assert (np.abs(img.astype(int) - np.array(g["image"])) <= 1).all()
+
+
+def test_curve_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
+    """Curves in the BVH (boxes = control points +- width/2, t range widened
+    for |dir| < 1 rays, Q10) give the flat list's image bit for bit."""
+    nx, ny, spp = 64, 36, 2
+    monkeypatch.setenv("RTAMD_BVH_MIN", "1000000000")
+    a = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.cornell_curves_small(nx, ny), nx, ny, 0, spp, SEED, a)
+    monkeypatch.setenv("RTAMD_BVH_MIN", "1")
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.cornell_curves_small(nx, ny), nx, ny, 0, spp, SEED, b)
+    assert np.array_equal(a, b)
+
+
+def test_curves_c5_scale(gpu_ctx, oracle_mod):
+    """Config C5's scene (2^20 curves in a BVH) at 1920x1080: a band of
+    pixels against the oracle.  The oracle walks the curves as a flat list,
+    so only a few pixels are checked, at 1 spp, on the rows where the band
+    meets the curve cloud."""
+    nx, ny = 1920, 1080
+    sc = scenes.cornell_curves(nx, ny)
+    acc = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, 1, SEED, acc)
+    assert np.isfinite(acc).all()
+    o = oracle_mod.build_scene(sc)
+    pix = np.array([540 * nx + x for x in range(900, 1020, 15)], dtype=np.uint32)
+    ref = np.zeros(nx * ny * 3)
+    o.render_pixels(nx, ny, 0, 1, SEED, ref, pix, nthreads=os.cpu_count() or 1)
+    for j in pix:
+        assert np.abs(acc[3 * j:3 * j + 3] - ref[3 * j:3 * j + 3]).max() <= 1e-9, j
