@@ -235,14 +235,41 @@ __device__ __forceinline__ double dot2d(const v3 a, const v3 b) { return (a.x * 
 
 struct BezFrame { Bez4 c; double v0; int depth; };
 
-// Returns true and the curve's t if it reports a hit for t-max `tmax`.
-__device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
-    const double w1 = B.w1, w2 = B.w2;
-    Bez4 c;
+__device__ __forceinline__ void bez_load(const BezierRec& B, const BezRay& R, Bez4& c) {   // bezier-transform :99-105
     c.p0 = bez_xf(R, B.cp[0], B.cp[1], B.cp[2]);
     c.p1 = bez_xf(R, B.cp[3], B.cp[4], B.cp[5]);
     c.p2 = bez_xf(R, B.cp[6], B.cp[7], B.cp[8]);
     c.p3 = bez_xf(R, B.cp[9], B.cp[10], B.cp[11]);
+}
+// bounding-box cull of converge (:123-128) against the ray-space cylinder
+__device__ __forceinline__ bool bez_culled(const Bez4& c, const double w1, const double t) {
+    const double zmn = fmin(fmin(c.p0.z, c.p1.z), fmin(c.p2.z, c.p3.z)) - w1;
+    const double zmx = fmax(fmax(c.p0.z, c.p1.z), fmax(c.p2.z, c.p3.z)) + w1;
+    const double xmn = fmin(fmin(c.p0.x, c.p1.x), fmin(c.p2.x, c.p3.x)) - w1;
+    const double xmx = fmax(fmax(c.p0.x, c.p1.x), fmax(c.p2.x, c.p3.x)) + w1;
+    const double ymn = fmin(fmin(c.p0.y, c.p1.y), fmin(c.p2.y, c.p3.y)) - w1;
+    const double ymx = fmax(fmax(c.p0.y, c.p1.y), fmax(c.p2.y, c.p3.y)) + w1;
+    return zmn >= t || zmx <= 0.000001 || xmn >= w1 || xmx <= -w1 || ymn >= w1 || ymx <= -w1;
+}
+// the whole curve's cull: false => converge reports no hit for this t-max
+__device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay& R, const double tmax) {
+    Bez4 c;
+    bez_load(B, R, c);
+    return !bez_culled(c, B.w1, tmax);
+}
+
+// Returns true and the curve's t if it reports a hit for t-max `tmax`.
+//
+// The answer does not depend on the order of the recursion: a leaf hit at
+// z <= tmax lies on its sub-curve, inside every ancestor's box, so no
+// ancestor culls it and converge's result is min z over all leaf hits with
+// z <= tmax.  The walk below therefore also culls with the best z found so
+// far (it cannot hide a smaller z), which only removes work.
+__device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
+    const double w1 = B.w1, w2 = B.w2;
+    Bez4 c;
+    bez_load(B, R, c);
+    if (bez_culled(c, w1, tmax)) return false;
     // flatness -> subdivision depth (:180-193)
     double l0 = -kTmax;
     {
@@ -260,16 +287,10 @@ __device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, co
     int sp = 0;
     double v0 = 0.0;
     int depth = maxd;
+    bool root = true;
     for (;;) {
-        // bounding-box cull (:123-128)
-        const double zmn = fmin(fmin(c.p0.z, c.p1.z), fmin(c.p2.z, c.p3.z)) - w1;
-        const double zmx = fmax(fmax(c.p0.z, c.p1.z), fmax(c.p2.z, c.p3.z)) + w1;
-        const double xmn = fmin(fmin(c.p0.x, c.p1.x), fmin(c.p2.x, c.p3.x)) - w1;
-        const double xmx = fmax(fmax(c.p0.x, c.p1.x), fmax(c.p2.x, c.p3.x)) + w1;
-        const double ymn = fmin(fmin(c.p0.y, c.p1.y), fmin(c.p2.y, c.p3.y)) - w1;
-        const double ymx = fmax(fmax(c.p0.y, c.p1.y), fmax(c.p2.y, c.p3.y)) + w1;
-        const bool culled = zmn >= tmax || zmx <= 0.000001 || xmn >= w1 || xmx <= -w1 || ymn >= w1 || ymx <= -w1;
-        if (!culled) {
+        if (root || !bez_culled(c, w1, best)) {
+            root = false;
             const double span = ldexp(1.0, depth - maxd);       // vn - v0 at this level
             if (depth >= 0) {                                   // split, left first (:167-175)
                 Bez4 l, r;
@@ -310,6 +331,83 @@ __device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, co
     return true;
 }
 
+// ------------------------------------------------- curve candidate batching
+// Curve tests are long and their length varies per (ray, curve), so testing
+// a curve in the lane that reached its BVH leaf leaves most of the wave idle.
+// Instead the lanes of a wave traverse independently and append (curve,
+// owner lane) candidates to a wave-local LDS queue; when 64 have gathered the
+// wave tests them together: first the cheap root cull for every candidate,
+// then the full subdivision for the survivors only, each lane taking one
+// pair.  Per owner the smallest z wins (ties: smallest curve index).  A
+// curve's answer does not depend on the t-max it is tested with, beyond
+// being reported only when z <= t-max (see bezier_test), so deferring the
+// tests changes no result.
+constexpr int kBezQ = 64 + 2 * 64;
+struct BezWave {
+    BezRay ray[64];                 // owner lane's ray-space matrix
+    double cl[64];                  // owner's closest t when the batch runs
+    double hz[64];                  // owner's best curve z from the batch
+    uint32_t hid[64];               // and its curve index
+    uint32_t q[kBezQ];              // candidates: curve << 6 | owner
+    uint32_t sv[kBezQ];             // root-test survivors
+    double sz[kBezQ];               // survivor results (z or +inf)
+};
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Runs the queued candidates; every active lane calls it (wave-uniform qn).
+__device__ __noinline__ void bez_flush(const DevScene& sc, BezWave& W, const uint32_t qn) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
+    // stage A: root cull
+    uint32_t sn = 0;
+    for (uint32_t base = 0; base < qn; base += nact) {
+        const uint32_t i = base + rank;
+        bool keep = false;
+        uint32_t e = 0;
+        if (i < qn) {
+            e = W.q[i];
+            keep = bez_root_passes(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) W.sv[sn + lanes_below(m)] = e;
+        sn += (uint32_t)__popcll(m);
+    }
+    wave_sync();
+    // stage B: subdivision for the survivors
+    for (uint32_t base = 0; base < sn; base += nact) {
+        const uint32_t i = base + rank;
+        if (i < sn) {
+            const uint32_t e = W.sv[i];
+            double t;
+            W.sz[i] = bezier_test(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], t) ? t : INFINITY;
+        }
+    }
+    wave_sync();
+    // per owner: min z, then the smallest curve index at that z
+    for (uint32_t base = 0; base < sn; base += nact) {
+        const uint32_t i = base + rank;
+        if (i < sn && W.sz[i] != INFINITY) {
+            const uint32_t o = W.sv[i] & 63u;
+            atomicMin((unsigned long long*)&W.hz[o], (unsigned long long)__double_as_longlong(W.sz[i]));
+        }
+    }
+    wave_sync();
+    for (uint32_t base = 0; base < sn; base += nact) {
+        const uint32_t i = base + rank;
+        if (i < sn && W.sz[i] != INFINITY) {
+            const uint32_t e = W.sv[i], o = e & 63u;
+            if (W.sz[i] == W.hz[o]) atomicMin(&W.hid[o], e >> 6);
+        }
+    }
+    wave_sync();
+}
+
 // Per-lane BVH traversal: every lane walks its own path through the BVH2
 // (child boxes tested at the parent, nearer child first, LDS stack with a
 // block-size stride so a wave's pushes hit 64 consecutive banks).
@@ -323,20 +421,11 @@ __device__ __forceinline__ bool box_hit_t(const double* bx, const v3 o, const v3
     return tnear <= tfar;
 }
 
-template <bool BEZ>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
     const double a = dot(d, d);
     const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
-    // A curve reports t as a distance along unit(d) (Q10), i.e. raw ray
-    // parameter t/|d|: for |d| < 1 the box range must reach closest/|d|.
-    double tscale = 1.0;
-    BezRay R;
-    if (BEZ && sc.bvh_has_bez) {
-        tscale = fmax(1.0, 1.0 / sqrt(a));
-        bez_ray(o, d, R);
-    }
     const uint32_t stride = blockDim.x;
     int sp = 0;
     int32_t node = sc.bvh2_root;
@@ -344,8 +433,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
         if (node >= 0) {
             const BvhNode2 N = sc.bvh2[node];
             double tl, tr;
-            const bool hl = box_hit_t(N.lbox, o, inv, closest * tscale, tl);
-            const bool hr = box_hit_t(N.rbox, o, inv, closest * tscale, tr);
+            const bool hl = box_hit_t(N.lbox, o, inv, closest, tl);
+            const bool hr = box_hit_t(N.rbox, o, inv, closest, tr);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
                 if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
@@ -366,16 +455,98 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
             }
-            if (BEZ) {
-                for (int s = L.bb; s < L.bb + L.bn; ++s) {
-                    double t;
-                    if (bezier_test(sc.bez[s], R, closest, t)) { closest = t; best = sc.leaf_base[LEAF_BEZIER] + s; }
-                }
-            }
         }
         if (sp == 0) break;
         --sp;
         node = (int32_t)lstk[sp * stride];
+    }
+}
+
+// Per-lane traversal of a BVH that holds curves: spheres are tested on the
+// spot, curves are queued and tested wave-wide (BezWave).  One BVH step per
+// loop iteration, so the wave checks the queue between steps.  A curve
+// reports t as a distance along unit(d) (Q10), i.e. raw ray parameter
+// t/|d|: for |d| < 1 the box range must reach closest/|d|.
+__device__ __noinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, const v3 d, const double time,
+                                                double& closest, int32_t& best, uint32_t* lstk, const int lmax,
+                                                BezWave& W) {
+    const double a = dot(d, d);
+    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
+    const double tscale = fmax(1.0, 1.0 / sqrt(a));
+    const uint32_t lane = threadIdx.x & 63u;
+    bez_ray(o, d, W.ray[lane]);
+    const uint32_t stride = blockDim.x;
+    int sp = 0;
+    int32_t node = sc.bvh2_root;
+    bool trav = true;
+    int pb = 0, pe = 0;                         // this lane's curves still to queue
+    uint32_t qn = 0;
+    for (;;) {
+        if (pb >= pe && trav) {                 // lanes with curves pending only queue them below
+            if (node >= 0) {
+                const BvhNode2 N = sc.bvh2[node];
+                double tl, tr;
+                const bool hl = box_hit_t(N.lbox, o, inv, closest * tscale, tl);
+                const bool hr = box_hit_t(N.rbox, o, inv, closest * tscale, tr);
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                    node = lfirst ? N.l : N.r;
+                } else if (hl) {
+                    node = N.l;
+                } else if (hr) {
+                    node = N.r;
+                } else if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
+            } else {
+                const BvhLeaf L = sc.bleaf[~node];
+                for (int s = L.sb; s < L.sb + L.sn; ++s) {
+                    const SphereRec S = sc.sph[s];
+                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                }
+                for (int s = L.mb; s < L.mb + L.mn; ++s) {
+                    const MSphereRec S = sc.msph[s];
+                    const double frac = (time - S.t0) / S.den;
+                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                }
+                pb = L.bb; pe = L.bb + L.bn;
+                if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
+            }
+        }
+        // append this step's curve candidates (at most 2 per lane)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool has = pb < pe;
+            const unsigned long long m = __ballot(has);
+            if (has) { W.q[qn + lanes_below(m)] = ((uint32_t)pb << 6) | lane; ++pb; }
+            qn += (uint32_t)__popcll(m);
+        }
+        const bool more = __ballot(trav || pb < pe) != 0ull;
+        if (qn >= 64u || (!more && qn > 0u)) {
+            W.cl[lane] = closest;
+            W.hz[lane] = INFINITY;
+            W.hid[lane] = 0xFFFFFFFFu;
+            wave_sync();
+            bez_flush(sc, W, qn);
+            qn = 0;
+            if (W.hid[lane] != 0xFFFFFFFFu) {     // a curve hit, z <= closest by construction
+                closest = W.hz[lane];
+                best = bz + (int32_t)W.hid[lane];
+            }
+            wave_sync();
+        }
+        if (!more) break;
     }
 }
 
@@ -387,13 +558,14 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 template <bool BEZ>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
                                                const double time, double& closest, uint32_t* lstk,
-                                               const int lmax) {
+                                               const int lmax, BezWave* bw) {
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
         const Group G = sc.groups[g];
         if (G.type == GROUP_BVH) {
-            bvh_closest_lane<BEZ>(sc, o0, d0, time, closest, best, lstk, lmax);
+            if (BEZ && sc.bvh_has_bez) bvh_closest_curves(sc, o0, d0, time, closest, best, lstk, lmax, *bw);
+            else bvh_closest_lane(sc, o0, d0, time, closest, best, lstk, lmax);
             continue;
         }
         v3 o = o0, d = d0;
@@ -548,6 +720,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts) {
     __shared__ uint32_t s_lstack[256 * LS];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
+    __shared__ BezWave s_bw[BEZ ? 4 : 1];
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     int cls = -1;
     uint32_t i = 0;
@@ -556,7 +729,8 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
         const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
         double t;
-        const int32_t leaf = closest_hit<BEZ>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS);
+        const int32_t leaf = closest_hit<BEZ>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS,
+                                              &s_bw[BEZ ? (threadIdx.x >> 6) : 0]);
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             const uint32_t wid = st.wid[i];
@@ -799,6 +973,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
                                                 unsigned long long* __restrict__ seg_count) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_lstack[256 * LS];
+    __shared__ BezWave s_bw[BEZ ? 4 : 1];
     stage_perlin(sc, P);
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     uint32_t segs = 0;
@@ -809,7 +984,8 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
         for (;;) {
             double t;
             ++segs;
-            const int32_t leaf = closest_hit<BEZ>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS);
+            const int32_t leaf = closest_hit<BEZ>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
+                                                  &s_bw[BEZ ? (threadIdx.x >> 6) : 0]);
             if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
             if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
         }
