@@ -233,7 +233,6 @@ __device__ __forceinline__ v3 bez_tan(const Bez4& c, const bool one) {         /
 }
 __device__ __forceinline__ double dot2d(const v3 a, const v3 b) { return (a.x * b.x + a.y * b.y) + 0.0 * 0.0; }
 
-struct BezFrame { Bez4 c; double v0; int depth; };
 
 __device__ __forceinline__ void bez_load(const BezierRec& B, const BezRay& R, Bez4& c) {   // bezier-transform :99-105
     c.p0 = bez_xf(R, B.cp[0], B.cp[1], B.cp[2]);
@@ -265,7 +264,7 @@ __device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay
 // ancestor culls it and converge's result is min z over all leaf hits with
 // z <= tmax.  The walk below therefore also culls with the best z found so
 // far (it cannot hide a smaller z), which only removes work.
-__device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
+__device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
     const double w1 = B.w1, w2 = B.w2;
     Bez4 c;
     bez_load(B, R, c);
@@ -283,24 +282,36 @@ __device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, co
     if (maxd > kBezMaxDepth) maxd = kBezMaxDepth;   // beyond any width / extent ratio a scene uses
     bool found = false;
     double best = tmax;
-    BezFrame stk[kBezMaxDepth + 1];
-    int sp = 0;
-    double v0 = 0.0;
-    int depth = maxd;
-    bool root = true;
+    // Depth-first walk of the subdivision tree without a stack: node (L, idx)
+    // is the sub-curve reached from the root by L splits at 0.5 taking the
+    // halves given by idx's bits (MSB first); its parameter range is
+    // [idx, idx + 1] * 2^-L.  Moving to a right sibling re-derives the node by
+    // the same split sequence from the root, so every sub-curve carries the
+    // exact values the reference's recursion computes.
+    const Bez4 root = c;
+    const int leaf_level = maxd + 1;            // converge's depth < 0 (root level has depth maxd)
+    int L = 0;
+    uint32_t idx = 0;
+    bool fresh = true;
     for (;;) {
-        if (root || !bez_culled(c, w1, best)) {
-            root = false;
-            const double span = ldexp(1.0, depth - maxd);       // vn - v0 at this level
-            if (depth >= 0) {                                   // split, left first (:167-175)
+        if (!fresh) {
+            c = root;
+            for (int k = L - 1; k >= 0; --k) {
                 Bez4 l, r;
                 bez_split(c, l, r);
-                stk[sp].c = r; stk[sp].v0 = v0 + span * 0.5; stk[sp].depth = depth - 1; ++sp;
-                c = l; depth -= 1;
+                c = ((idx >> k) & 1u) ? r : l;
+            }
+        }
+        fresh = false;
+        if (!bez_culled(c, w1, best)) {
+            if (L < leaf_level) {                               // split, left first (:167-175)
+                Bez4 l, r;
+                bez_split(c, l, r);
+                c = l; ++L; idx <<= 1; fresh = true;
                 continue;
             }
             // leaf segment (:130-166)
-            const double vn = v0 + span;
+            const double v0 = ldexp((double)idx, -L), vn = v0 + ldexp(1.0, -L);
             const v3 dir = c.p3 - c.p0;
             v3 dp0 = bez_tan(c, false);
             if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
@@ -322,9 +333,9 @@ __device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, co
                 }
             }
         }
-        if (sp == 0) break;
-        --sp;
-        c = stk[sp].c; v0 = stk[sp].v0; depth = stk[sp].depth;
+        while (L > 0 && (idx & 1u)) { --L; idx >>= 1; }          // climb past right children
+        if (L == 0) break;
+        ++idx;                                                  // right sibling
     }
     if (!(found && kTmin < best)) return false;                 // :201
     tout = best;
@@ -342,15 +353,16 @@ __device__ __noinline__ bool bezier_test(const BezierRec& B, const BezRay& R, co
 // curve's answer does not depend on the t-max it is tested with, beyond
 // being reported only when z <= t-max (see bezier_test), so deferring the
 // tests changes no result.
-constexpr int kBezQ = 64 + 2 * 64;
+constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
+constexpr int kBezS = 64 + kBezQ;     // survivors: < 64 carried over + one stage A's worth
 struct BezWave {
     BezRay ray[64];                 // owner lane's ray-space matrix
-    double cl[64];                  // owner's closest t when the batch runs
+    double cl[64];                  // owner's closest t when a batch runs
     double hz[64];                  // owner's best curve z from the batch
     uint32_t hid[64];               // and its curve index
     uint32_t q[kBezQ];              // candidates: curve << 6 | owner
-    uint32_t sv[kBezQ];             // root-test survivors
-    double sz[kBezQ];               // survivor results (z or +inf)
+    uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
+    double sz[kBezS];               // their results (z or +inf)
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -360,12 +372,12 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Runs the queued candidates; every active lane calls it (wave-uniform qn).
-__device__ __noinline__ void bez_flush(const DevScene& sc, BezWave& W, const uint32_t qn) {
+// Stage A: root cull of the qn queued candidates; survivors are appended to
+// the survivor list (svn entries already there).  Returns the new count.
+// Every active lane calls it with the same arguments.
+__device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, const uint32_t qn, uint32_t svn) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
-    // stage A: root cull
-    uint32_t sn = 0;
     for (uint32_t base = 0; base < qn; base += nact) {
         const uint32_t i = base + rank;
         bool keep = false;
@@ -375,36 +387,47 @@ __device__ __noinline__ void bez_flush(const DevScene& sc, BezWave& W, const uin
             keep = bez_root_passes(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
         }
         const unsigned long long m = __ballot(keep);
-        if (keep) W.sv[sn + lanes_below(m)] = e;
-        sn += (uint32_t)__popcll(m);
+        if (keep) W.sv[svn + lanes_below(m)] = e;
+        svn += (uint32_t)__popcll(m);
     }
     wave_sync();
-    // stage B: subdivision for the survivors
-    for (uint32_t base = 0; base < sn; base += nact) {
+    return svn;
+}
+
+// Stage B: full subdivision of the first nb survivors, one per lane, then per
+// owner the smallest z (ties: smallest curve index) into hz / hid; the
+// remaining svn - nb survivors move to the front.
+__device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn) {
+    const unsigned long long act = __ballot(1);
+    const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
+    for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
-        if (i < sn) {
+        if (i < nb) {
             const uint32_t e = W.sv[i];
             double t;
             W.sz[i] = bezier_test(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], t) ? t : INFINITY;
         }
     }
     wave_sync();
-    // per owner: min z, then the smallest curve index at that z
-    for (uint32_t base = 0; base < sn; base += nact) {
+    for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
-        if (i < sn && W.sz[i] != INFINITY) {
-            const uint32_t o = W.sv[i] & 63u;
-            atomicMin((unsigned long long*)&W.hz[o], (unsigned long long)__double_as_longlong(W.sz[i]));
-        }
+        if (i < nb && W.sz[i] != INFINITY)
+            atomicMin((unsigned long long*)&W.hz[W.sv[i] & 63u], (unsigned long long)__double_as_longlong(W.sz[i]));
     }
     wave_sync();
-    for (uint32_t base = 0; base < sn; base += nact) {
+    for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
-        if (i < sn && W.sz[i] != INFINITY) {
+        if (i < nb && W.sz[i] != INFINITY) {
             const uint32_t e = W.sv[i], o = e & 63u;
             if (W.sz[i] == W.hz[o]) atomicMin(&W.hid[o], e >> 6);
         }
     }
+    wave_sync();
+    const uint32_t rest = svn - nb;             // < nact <= 64, disjoint from [0, rest) only if nb >= rest
+    uint32_t e = 0;
+    if (rank < rest) e = W.sv[nb + rank];
+    wave_sync();
+    if (rank < rest) W.sv[rank] = e;
     wave_sync();
 }
 
@@ -467,7 +490,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 // loop iteration, so the wave checks the queue between steps.  A curve
 // reports t as a distance along unit(d) (Q10), i.e. raw ray parameter
 // t/|d|: for |d| < 1 the box range must reach closest/|d|.
-__device__ __noinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, const v3 d, const double time,
+__device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
                                                 BezWave& W) {
     const double a = dot(d, d);
@@ -481,7 +504,7 @@ __device__ __noinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, 
     int32_t node = sc.bvh2_root;
     bool trav = true;
     int pb = 0, pe = 0;                         // this lane's curves still to queue
-    uint32_t qn = 0;
+    uint32_t qn = 0, svn = 0;                   // queued candidates, survivors awaiting subdivision
     for (;;) {
         if (pb >= pe && trav) {                 // lanes with curves pending only queue them below
             if (node >= 0) {
@@ -533,18 +556,25 @@ __device__ __noinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, 
             qn += (uint32_t)__popcll(m);
         }
         const bool more = __ballot(trav || pb < pe) != 0ull;
-        if (qn >= 64u || (!more && qn > 0u)) {
+        if (qn >= 64u || (!more && (qn > 0u || svn > 0u))) {
             W.cl[lane] = closest;
-            W.hz[lane] = INFINITY;
-            W.hid[lane] = 0xFFFFFFFFu;
             wave_sync();
-            bez_flush(sc, W, qn);
+            svn = bez_stage_a(sc, W, qn, svn);
             qn = 0;
-            if (W.hid[lane] != 0xFFFFFFFFu) {     // a curve hit, z <= closest by construction
-                closest = W.hz[lane];
-                best = bz + (int32_t)W.hid[lane];
+            const uint32_t nact = (uint32_t)__popcll(__ballot(1));
+            const uint32_t nb = more ? svn - svn % nact : svn;
+            if (nb > 0u) {
+                W.hz[lane] = INFINITY;
+                W.hid[lane] = 0xFFFFFFFFu;
+                wave_sync();
+                bez_stage_b(sc, W, nb, svn);
+                svn -= nb;
+                if (W.hid[lane] != 0xFFFFFFFFu && W.hz[lane] <= closest) {   // z <= the t-max it was tested with
+                    closest = W.hz[lane];
+                    best = bz + (int32_t)W.hid[lane];
+                }
+                wave_sync();
             }
-            wave_sync();
         }
         if (!more) break;
     }
