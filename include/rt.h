@@ -85,6 +85,11 @@ int rt_add_bezier(int scene, const double a[3], const double b[3], const double 
  * (a,b,c,d per curve); the curves get the consecutive object ids *out_first .. *out_first + n - 1 */
 int rt_add_bezier_array(int scene, const double* cps, int n, double width, int mat, int* out_first);
 int rt_add_flip_normals(int scene, int obj, int* out_obj);                                       /* g:flip-normals :433 */
+/* g:make-constant-medium boundary density a (geometry.scm:545): a volume of the given density inside
+ * `boundary` (spheres / rects / boxes / instances); the phase function is a lambertian material with
+ * texture albedo_tex, created by this call.  Its hit test draws one random number (like the reference),
+ * so media are evaluated in object-list order relative to the objects before them. */
+int rt_add_constant_medium(int scene, int boundary, double density, int albedo_tex, int* out_obj);
 int rt_add_box(int scene, const double p0[3], const double p1[3], int mat, int* out_obj);       /* g:make-box :444 */
 int rt_add_translate(int scene, int obj, const double offset[3], int* out_obj);                 /* g:translate :465 */
 int rt_add_rotate_y(int scene, int obj, double angle_deg, int* out_obj);                        /* g:rotate-y :483 */

@@ -112,7 +112,7 @@ static inline v3 point_at(ray_t r, double t) { return vadd(r.o, vscale(r.d, t));
 enum { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum { OBJ_SPHERE = 0, OBJ_MOVING_SPHERE, OBJ_RECT, OBJ_FLIP, OBJ_BOX, OBJ_TRANSLATE,
-       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH, OBJ_BEZIER };
+       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH, OBJ_BEZIER, OBJ_MEDIUM };
 
 typedef struct { int type, a, b; v3 rgb; double scale; } orc_tex;
 typedef struct { int type, tex; double fuzz, ref_idx; } orc_mat;
@@ -126,6 +126,7 @@ typedef struct {
     int box_list;                       /* OBJ_BOX: its 6-rect list object */
     v3 cp[4];                           /* OBJ_BEZIER control points */
     double width;
+    double density;                     /* OBJ_MEDIUM (child = boundary, mat = phase lambertian) */
 } orc_obj;
 
 typedef struct {
@@ -265,6 +266,13 @@ int orc_add_bezier(orc_scene* s, const double* cps, double width, int mat) {
     int i = new_obj(s, OBJ_BEZIER);
     for (int k = 0; k < 4; ++k) s->obj[i].cp[k] = V(cps[3 * k], cps[3 * k + 1], cps[3 * k + 2]);
     s->obj[i].width = width; s->obj[i].mat = mat;
+    return i;
+}
+
+int orc_add_constant_medium(orc_scene* s, int boundary, double density, int tex) {
+    int phase = orc_add_material_lambertian(s, tex);     /* (m:make-lambertian a), geometry.scm:546 */
+    int i = new_obj(s, OBJ_MEDIUM);
+    s->obj[i].child = boundary; s->obj[i].density = density; s->obj[i].mat = phase;
     return i;
 }
 
@@ -557,6 +565,10 @@ static int bezier_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitre
 
 static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec);
 
+/* The path's random stream, for hit functions that draw (the constant
+ * medium, geometry.scm:564): set by color() around each world hit. */
+static __thread orc_rng* tl_rng;
+
 static int hit_list(const orc_scene* s, int first, int count, ray_t r, double tmin, double tmax,
                     hitrec* rec) {                                      /* :33-50 */
     int hit_anything = 0;
@@ -652,6 +664,26 @@ static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax
         return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
     case OBJ_BEZIER:
         return bezier_hit(o, r, tmin, tmax, rec);
+    case OBJ_MEDIUM: {                                                  /* :545-578 */
+        hitrec r1, r2;
+        if (!hit_obj(s, o->child, r, -ORC_TMAX, ORC_TMAX, &r1)) return 0;
+        if (!hit_obj(s, o->child, r, r1.t + 0.0001, ORC_TMAX, &r2)) return 0;
+        double t1 = (r1.t < tmin) ? tmin : r1.t;
+        double t2 = (r2.t > tmax) ? tmax : r2.t;
+        if (t1 >= t2) return 0;
+        if (t1 < 0) t1 = 0;
+        double inside = (t2 - t1) * vlength(r.d);
+        if (!tl_rng) return 0;                    /* hit_world KATs: no path stream */
+        double hd = (-(1 / o->density)) * log(orc_random_real(tl_rng));
+        if (!(hd < inside)) return 0;
+        double nt = t1 + hd / vlength(r.d);
+        rec->t = nt;
+        rec->p = point_at(r, nt);
+        rec->n = V(1, 0, 0);
+        rec->mat = o->mat;
+        rec->u = 0; rec->v = 0;
+        return 1;
+    }
     }
     return 0;
 }
@@ -725,7 +757,10 @@ static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters
     const orc_obj* w = &s->obj[s->world];
     cnt->segments++;
     if (depth > cnt->max_depth) cnt->max_depth = depth;
-    if (!hit_list(s, w->first, w->count, r, ORC_TMIN, ORC_TMAX, &rec)) return sky(s, r);
+    tl_rng = g;
+    int hit = hit_list(s, w->first, w->count, r, ORC_TMIN, ORC_TMAX, &rec);
+    tl_rng = 0;
+    if (!hit) return sky(s, r);
     const orc_mat* m = &s->mat[rec.mat];
     switch (m->type) {
     case MAT_LAMBERTIAN: {                                              /* material.scm:24-39 */

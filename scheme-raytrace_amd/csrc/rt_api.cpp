@@ -45,7 +45,7 @@ int fail(const std::string& msg) { g_err = msg; return 1; }
     } while (0)
 
 // ------------------------------------------------------------- objects
-enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH, O_BEZIER };
+enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH, O_BEZIER, O_MEDIUM };
 
 struct Obj {
     ObjType type;
@@ -94,7 +94,7 @@ struct Scene {
 
     // flattened + uploaded
     DevScene dev{};
-    DevBuf d_sph, d_msph, d_rect, d_bez, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
+    DevBuf d_sph, d_msph, d_rect, d_bez, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     // render buffers
     DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
     uint32_t* h_counts = nullptr;     // pinned
@@ -149,14 +149,17 @@ struct LeafTmp {
     int chain;         // -1 = world
     int flip;
     int obj;           // source object
+    int aux = -1;      // LEAF_MEDIUM: index into Flattener::bounds
 };
 
 struct Flattener {
     Scene* s;
     std::vector<std::vector<ChainOpRec>> chains;   // unique chains
     std::vector<LeafTmp> leaves;                   // DFS order
+    std::vector<std::vector<LeafTmp>> bounds;      // per constant medium: its boundary's leaves
     std::vector<ChainOpRec> cur;
     int depth_guard = 0;
+    bool in_boundary = false;
 
     int chain_id() {
         if (cur.empty()) return -1;
@@ -176,7 +179,27 @@ struct Flattener {
         case O_SPHERE: leaves.push_back({LEAF_SPHERE, chain_id(), flip, id}); break;
         case O_MSPHERE: leaves.push_back({LEAF_MSPHERE, chain_id(), flip, id}); break;
         case O_RECT: leaves.push_back({LEAF_RECT_XY + o.axis, chain_id(), flip, id}); break;
-        case O_BEZIER: leaves.push_back({LEAF_BEZIER, chain_id(), flip, id}); break;
+        case O_BEZIER:
+            if (in_boundary) return fail("a constant medium's boundary may hold spheres, rects, boxes and instances only");
+            leaves.push_back({LEAF_BEZIER, chain_id(), flip, id});
+            break;
+        case O_MEDIUM: {
+            if (in_boundary) return fail("constant media cannot be nested");
+            std::vector<LeafTmp> saved;
+            saved.swap(leaves);
+            in_boundary = true;
+            rc = walk(o.child, 0);
+            in_boundary = false;
+            std::vector<LeafTmp> b;
+            b.swap(leaves);
+            leaves.swap(saved);
+            if (rc) break;
+            bounds.push_back(std::move(b));
+            LeafTmp L{LEAF_MEDIUM, chain_id(), flip, id};
+            L.aux = (int)bounds.size() - 1;
+            leaves.push_back(L);
+            break;
+        }
         case O_FLIP: rc = walk(o.child, flip ^ 1); break;
         case O_BOX:
         case O_LIST:
@@ -341,11 +364,24 @@ int commit_scene(Scene* s, int world) {
         return b;
     };
 
-    // BVH over the world-level (chain -1) spheres, moving spheres and curves
+    // A constant medium draws a random number inside its hit test, so its
+    // position in the object list matters (the draw happens only if the
+    // closest hit so far leaves part of its span): the leaves are cut into
+    // segments at each medium and evaluated segment by segment, each medium
+    // right after the objects that precede it.  Within a segment the order of
+    // the other primitives does not change the closest hit.
+    std::vector<int> seg(f.leaves.size(), 0);
+    int nseg = 1;
+    for (size_t i = 0; i < f.leaves.size(); ++i) {
+        seg[i] = nseg - 1;
+        if (f.leaves[i].type == LEAF_MEDIUM) ++nseg;
+    }
+
+    // BVH over the world-level (chain -1) spheres, moving spheres and curves of segment 0
     std::vector<PrimRef> refs;
     for (size_t i = 0; i < f.leaves.size(); ++i) {
         const LeafTmp& L = f.leaves[i];
-        if (L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE && L.type != LEAF_BEZIER)) continue;
+        if (seg[i] != 0 || L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE && L.type != LEAF_BEZIER)) continue;
         const Obj& o = s->objs[L.obj];
         PrimRef r{};
         r.leaf = (int)i;
@@ -451,51 +487,84 @@ int commit_scene(Scene* s, int world) {
             }
         }
     }
-    for (int ch : chain_order) {
-        for (int type = LEAF_SPHERE; type <= LEAF_BEZIER; ++type) {
-            if (use_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE || type == LEAF_BEZIER)) continue;
-            Group g{type, ch, 0, 0};
-            auto type_size = [&]() {
-                return (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size()
-                     : (type == LEAF_BEZIER) ? bez.size() : rect.size();
-            };
-            size_t before = type_size();
-            g.begin = (int)before;
-            for (const LeafTmp& L : f.leaves) {
-                if (L.chain != ch || L.type != type) continue;
-                const Obj& o = s->objs[L.obj];
-                LeafInfo li{};
-                li.type = type; li.group = (int)groups.size(); li.mat = o.mat; li.flip = L.flip;
-                if (type == LEAF_SPHERE) {
-                    li.local = (int)sph.size();
-                    sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
-                    li.inv_r = 1.0 / o.r; li.radius = o.r;
-                    lsph.push_back(li);
-                } else if (type == LEAF_MSPHERE) {
-                    li.local = (int)msph.size();
-                    MSphereRec m{};
-                    m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
-                    m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
-                    m.t0 = o.t0; m.den = o.t1 - o.t0;
-                    msph.push_back(m);
-                    li.inv_r = 1.0 / o.r; li.radius = o.r;
-                    lmsph.push_back(li);
-                } else if (type == LEAF_BEZIER) {
-                    li.local = (int)bez.size();
-                    bez.push_back(bezier_rec(o));
-                    lbez.push_back(li);
-                } else {
-                    li.local = (int)rect.size();
-                    RectRec r{};
-                    r.a0 = o.a0; r.a1 = o.a1; r.b0 = o.b0; r.b1 = o.b1; r.k = o.k;
-                    rect.push_back(r);
-                    lrect[type - LEAF_RECT_XY].push_back(li);
-                }
-            }
-            size_t after = type_size();
-            g.end = (int)after;
-            if (after > before) groups.push_back(g);
+    std::vector<MediumRec> med;
+    std::vector<LeafInfo> lmed;
+    std::vector<Group> bgroups;
+    // records of one leaf (boundary leaves get no LeafInfo: they are never a closest hit)
+    auto add_record = [&](const LeafTmp& L, LeafInfo* li) {
+        const Obj& o = s->objs[L.obj];
+        if (L.type == LEAF_SPHERE) {
+            if (li) { li->local = (int)sph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lsph.push_back(*li); }
+            sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
+        } else if (L.type == LEAF_MSPHERE) {
+            MSphereRec m{};
+            m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
+            m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
+            m.t0 = o.t0; m.den = o.t1 - o.t0;
+            if (li) { li->local = (int)msph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lmsph.push_back(*li); }
+            msph.push_back(m);
+        } else if (L.type == LEAF_BEZIER) {
+            if (li) { li->local = (int)bez.size(); lbez.push_back(*li); }
+            bez.push_back(bezier_rec(o));
+        } else {
+            RectRec r{};
+            r.a0 = o.a0; r.a1 = o.a1; r.b0 = o.b0; r.b1 = o.b1; r.k = o.k;
+            if (li) { li->local = (int)rect.size(); lrect[L.type - LEAF_RECT_XY].push_back(*li); }
+            rect.push_back(r);
         }
+    };
+    auto type_size = [&](int type) {
+        return (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size()
+             : (type == LEAF_BEZIER) ? bez.size() : rect.size();
+    };
+    // group a leaf subset by (chain, type) into `out`; world leaves also get LeafInfo
+    auto emit_groups = [&](const std::vector<const LeafTmp*>& ls, std::vector<Group>& out, bool world, bool skip_bvh) {
+        for (int ch : chain_order) {
+            for (int type = LEAF_SPHERE; type <= LEAF_BEZIER; ++type) {
+                if (skip_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE || type == LEAF_BEZIER)) continue;
+                Group g{type, ch, 0, 0};
+                const size_t before = type_size(type);
+                g.begin = (int)before;
+                for (const LeafTmp* L : ls) {
+                    if (L->chain != ch || L->type != type) continue;
+                    if (world) {
+                        LeafInfo li{};
+                        li.type = type; li.group = (int)out.size(); li.mat = s->objs[L->obj].mat; li.flip = L->flip;
+                        add_record(*L, &li);
+                    } else {
+                        add_record(*L, nullptr);
+                    }
+                }
+                const size_t after = type_size(type);
+                g.end = (int)after;
+                if (after > before) out.push_back(g);
+            }
+        }
+    };
+    for (int sg = 0; sg < nseg; ++sg) {
+        std::vector<const LeafTmp*> ls;
+        const LeafTmp* medium = nullptr;
+        for (size_t i = 0; i < f.leaves.size(); ++i) {
+            if (seg[i] != sg) continue;
+            if (f.leaves[i].type == LEAF_MEDIUM) medium = &f.leaves[i];
+            else ls.push_back(&f.leaves[i]);
+        }
+        emit_groups(ls, groups, true, use_bvh && sg == 0);
+        if (!medium) continue;
+        const Obj& o = s->objs[medium->obj];
+        MediumRec m{};
+        m.bg_begin = (int)bgroups.size();
+        std::vector<const LeafTmp*> bl;
+        for (const LeafTmp& L : f.bounds[medium->aux]) bl.push_back(&L);
+        emit_groups(bl, bgroups, false, false);
+        m.bg_end = (int)bgroups.size();
+        m.neg_inv_density = -(1 / o.r);             // (- (/ 1 density)), geometry.scm:564
+        LeafInfo li{};
+        li.type = LEAF_MEDIUM; li.group = (int)groups.size(); li.local = (int)med.size();
+        li.mat = o.mat; li.flip = medium->flip;
+        groups.push_back(Group{LEAF_MEDIUM, medium->chain, (int)med.size(), (int)med.size() + 1});
+        med.push_back(m);
+        lmed.push_back(li);
     }
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
     std::vector<LeafInfo> leaves;
@@ -512,6 +581,8 @@ int commit_scene(Scene* s, int world) {
     base[LEAF_RECT_XY] = base[LEAF_RECT_XZ] = base[LEAF_RECT_YZ] = rect_base;
     base[LEAF_BEZIER] = (int32_t)leaves.size();
     for (auto& li : lbez) leaves.push_back(li);
+    base[LEAF_MEDIUM] = (int32_t)leaves.size();
+    for (auto& li : lmed) leaves.push_back(li);
 
     std::vector<Chain> chains;
     for (auto& cv : f.chains) {
@@ -528,6 +599,10 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_groups, groups, &d.groups)) return rc;
     if (int rc = upload(s->d_bez, bez, &d.bez)) return rc;
     d.n_bez = (int)bez.size();
+    if (int rc = upload(s->d_med, med, &d.med)) return rc;
+    d.n_med = (int)med.size();
+    if (int rc = upload(s->d_bgroups, bgroups, &d.bgroups)) return rc;
+    d.n_bgroups = (int)bgroups.size();
     d.bvh_has_bez = bvh_has_bez ? 1 : 0;
     if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
@@ -905,6 +980,19 @@ int rt_add_bezier_array(int scene, const double* cps, int n, double width, int m
         s->objs.push_back(std::move(o));
     }
     return 0;
+}
+int rt_add_constant_medium(int scene, int boundary, double density, int albedo_tex, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (check_obj(s, boundary)) return 1;
+    if (check_tex(s, albedo_tex)) return 1;
+    if (!(density > 0.0) || !std::isfinite(density)) return fail("rt_add_constant_medium: density must be positive and finite");
+    // the phase function is (m:make-lambertian a), geometry.scm:546
+    DevMaterial m{};
+    m.type = MAT_LAMBERTIAN; m.tex = albedo_tex;
+    s->mats.push_back(m);
+    Obj o; o.type = O_MEDIUM; o.child = boundary; o.r = density; o.mat = (int)s->mats.size() - 1;
+    return push_obj(s, std::move(o), out);
 }
 int rt_add_flip_normals(int scene, int child, int* out) {
     SCENE_OR_FAIL(s, scene);

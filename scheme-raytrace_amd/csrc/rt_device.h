@@ -22,9 +22,11 @@ constexpr int kMaxChain = 4;                   // instance ops per leaf chain
 enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum LeafType : int32_t { LEAF_SPHERE = 0, LEAF_MSPHERE = 1, LEAF_RECT_XY = 2, LEAF_RECT_XZ = 3,
-                          LEAF_RECT_YZ = 4, LEAF_BEZIER = 5 };
-constexpr int kLeafTypes = 6;
-constexpr int32_t GROUP_BVH = 6;               // group type: BVH over world-level spheres / curves
+                          LEAF_RECT_YZ = 4, LEAF_BEZIER = 5, LEAF_MEDIUM = 6 };
+constexpr int kLeafTypes = 7;
+constexpr int32_t GROUP_BVH = 7;               // group type: BVH over world-level spheres / curves
+// closest-hit kernel variants: scene features compiled in
+constexpr int kFeatCurves = 1, kFeatMedia = 2;
 enum ChainOp : int32_t { OP_TRANSLATE = 0, OP_ROTATE_Y = 1 };
 
 struct DevTexture {            // texture.scm:12-34
@@ -48,6 +50,10 @@ struct alignas(64) RectRec { double a0, a1, b0, b1, k, pad0, pad1, pad2; };
 // width1 = width/2, width2 = width1^2, eps8 = 8*(width/20).
 struct alignas(64) BezierRec { double cp[12]; double w1, w2, eps8, pad; };
 constexpr int kBezMaxDepth = 24;               // subdivision levels the curve test supports
+// Constant medium (geometry.scm:545-578): its boundary is the closest hit over
+// the boundary groups [bg_begin, bg_end) of DevScene::bgroups; neg_inv_density
+// = (- (/ 1 density)).  The phase function is a lambertian material.
+struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density, pad; };
 
 // BVH over the world-level spheres, moving spheres and curves, per-lane
 // traversal layout (Aila & Laine style BVH2): both child boxes live in the
@@ -85,6 +91,8 @@ struct DevScene {
     const MSphereRec* msph; int32_t n_msph;
     const RectRec* rect;   int32_t n_rect;
     const BezierRec* bez;  int32_t n_bez;
+    const MediumRec* med;  int32_t n_med;
+    const Group* bgroups;  int32_t n_bgroups;     // medium boundaries (not part of the world loop)
     const Group* groups;   int32_t n_groups;
     const BvhNode2* bvh2;  int32_t n_bvh2;
     const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)

@@ -585,10 +585,88 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
 // (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
 // walks the same group / primitive sequence, so the primitive records are
 // fetched once per wave through the scalar unit.
-template <bool BEZ>
+// ------------------------------------------------------- constant medium
+// Closest boundary hit in (tmin, tmax) over a medium's boundary groups, with
+// the reference's hit semantics (spheres strict, rects non-strict).
+__device__ __forceinline__ bool boundary_hit(const DevScene& sc, const MediumRec& M, const v3 o0, const v3 d0,
+                                             const double time, const double tmin, const double tmax,
+                                             double& tout) {
+    double closest = tmax;
+    bool hit = false;
+    for (int g = M.bg_begin; g < M.bg_end; ++g) {
+        const Group G = sc.bgroups[g];
+        v3 o = o0, d = d0;
+        if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
+        if (G.type == LEAF_SPHERE || G.type == LEAF_MSPHERE) {
+            const double a = dot(d, d);
+            for (int s = G.begin; s < G.end; ++s) {
+                v3 c;
+                double rr;
+                if (G.type == LEAF_SPHERE) {
+                    const SphereRec S = sc.sph[s];
+                    c = mk(S.cx, S.cy, S.cz); rr = S.rr;
+                } else {
+                    const MSphereRec S = sc.msph[s];
+                    c = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * ((time - S.t0) / S.den);
+                    rr = S.rr;
+                }
+                const v3 oc = o - c;
+                const double b = dot(oc, d);
+                const double cc = dot(oc, oc) - rr;
+                const double disc = b * b - a * cc;
+                if (disc > 0.0) {
+                    const double sq = sqrt(disc);
+                    double t = (-b - sq) / a;
+                    if (!(tmin < t && t < closest)) t = (-b + sq) / a;
+                    if (tmin < t && t < closest) { closest = t; hit = true; }
+                }
+            }
+        } else {
+            double ok, dk, oa, da, ob, db;
+            if (G.type == LEAF_RECT_XY) { ok = o.z; dk = d.z; oa = o.x; da = d.x; ob = o.y; db = d.y; }
+            else if (G.type == LEAF_RECT_XZ) { ok = o.y; dk = d.y; oa = o.x; da = d.x; ob = o.z; db = d.z; }
+            else { ok = o.x; dk = d.x; oa = o.y; da = d.y; ob = o.z; db = d.z; }
+            for (int s = G.begin; s < G.end; ++s) {
+                const RectRec R = sc.rect[s];
+                const double t = (R.k - ok) / dk;
+                if (t < tmin || t > closest) continue;
+                const double A = oa + t * da, Bv = ob + t * db;
+                if (A < R.a0 || A > R.a1 || Bv < R.b0 || Bv > R.b1) continue;
+                closest = t; hit = true;
+            }
+        }
+    }
+    tout = closest;
+    return hit;
+}
+// make-constant-medium's hit (geometry.scm:547-575).  o0, d0 are the world
+// ray (boundary groups carry their full instance chain); d is the ray in the
+// medium's own space.  Draws one random number when the ray's span inside
+// the boundary overlaps (tmin, tmax), like the reference.
+__device__ __forceinline__ bool medium_test(const DevScene& sc, const MediumRec& M, const v3 o0, const v3 d0,
+                                            const v3 d, const double time, const double tmax, Rng& g,
+                                            double& tout) {
+    double t1r, t2r;
+    if (!boundary_hit(sc, M, o0, d0, time, -kTmax, kTmax, t1r)) return false;
+    if (!boundary_hit(sc, M, o0, d0, time, t1r + 0.0001, kTmax, t2r)) return false;
+    double t1 = (t1r < kTmin) ? kTmin : t1r;
+    const double t2 = (t2r > tmax) ? tmax : t2r;
+    if (t1 >= t2) return false;
+    if (t1 < 0.0) t1 = 0.0;
+    const double len = length(d);
+    const double inside = (t2 - t1) * len;
+    const double hd = M.neg_inv_density * log(g.next());
+    if (!(hd < inside)) return false;
+    tout = t1 + hd / len;
+    return true;
+}
+
+template <int F>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
                                                const double time, double& closest, uint32_t* lstk,
-                                               const int lmax, BezWave* bw) {
+                                               const int lmax, BezWave* bw, Rng* rng) {
+    constexpr bool BEZ = (F & kFeatCurves) != 0;
+    constexpr bool MED = (F & kFeatMedia) != 0;
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
@@ -619,6 +697,13 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
                 }
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
+            }
+        } else if (G.type == LEAF_MEDIUM) {                // geometry.scm:545-578
+            if (MED) {
+                for (int s = G.begin; s < G.end; ++s) {
+                    double t;
+                    if (medium_test(sc, sc.med[s], o0, d0, d, time, closest, *rng, t)) { closest = t; best = base + s; }
+                }
             }
         } else if (G.type == LEAF_BEZIER) {                // bezier.scm:176-214
             if (BEZ) {
@@ -743,13 +828,15 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
 // the spot (sky); hits are appended to the queue of their material type so
 // each shade kernel runs one material's code (wavefront material queues).
 // =====================================================================
-template <int LS, bool BEZ>
+template <int LS, int F>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                 uint32_t* __restrict__ queues, uint32_t qstride,
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts) {
     __shared__ uint32_t s_lstack[256 * LS];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
+    constexpr bool BEZ = (F & kFeatCurves) != 0;
+    constexpr bool MED = (F & kFeatMedia) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     int cls = -1;
@@ -759,8 +846,11 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
         const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
         double t;
-        const int32_t leaf = closest_hit<BEZ>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS,
-                                              &s_bw[BEZ ? (threadIdx.x >> 6) : 0]);
+        Rng g;
+        if (MED) g.init(rp.k0, rp.k1, st.pix[i], st.smp[i], st.rng[i]);
+        const int32_t leaf = closest_hit<F>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS,
+                                            &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g);
+        if (MED) st.rng[i] = g.ctr;                 // draws taken inside media
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             const uint32_t wid = st.wid[i];
@@ -866,8 +956,8 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         nrm = mk(0.0, 0.0, 1.0);
     } else if (li.type == LEAF_RECT_XZ) {
         nrm = mk(0.0, 1.0, 0.0);
-    } else if (li.type == LEAF_RECT_YZ) {
-        nrm = mk(1.0, 0.0, 0.0);
+    } else if (li.type == LEAF_RECT_YZ || li.type == LEAF_MEDIUM) {
+        nrm = mk(1.0, 0.0, 0.0);                             // medium: (v:vec3 1 0 0), geometry.scm:569
     } else {
         nrm = d * -1.0;                                      // curve: (v:scale (dir r) -1), bezier.scm:204
     }
@@ -997,12 +1087,14 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
-template <int LS, bool BEZ>
+template <int LS, int F>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ seg_count) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_lstack[256 * LS];
+    constexpr bool BEZ = (F & kFeatCurves) != 0;
+    constexpr bool MED = (F & kFeatMedia) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
     stage_perlin(sc, P);
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
@@ -1014,8 +1106,11 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
         for (;;) {
             double t;
             ++segs;
-            const int32_t leaf = closest_hit<BEZ>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
-                                                  &s_bw[BEZ ? (threadIdx.x >> 6) : 0]);
+            Rng g;
+            if (MED) g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
+            const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
+                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g);
+            if (MED) p.rng = g.ctr;
             if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
             if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
         }
@@ -1060,16 +1155,24 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     hipLaunchKernelGGL(k_raygen, dim3(blocks), dim3(256), 0, s, sc, rp, st);
     return hipGetLastError();
 }
+static int scene_features(const DevScene& sc) {
+    return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 ? kFeatMedia : 0);
+}
 hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
                          uint32_t* counts, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-#define RT_EXTEND(LS, BEZ)                                                                                   \
-    hipLaunchKernelGGL((k_extend<LS, BEZ>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,   \
+#define RT_EXTEND(LS, F)                                                                                     \
+    hipLaunchKernelGGL((k_extend<LS, F>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,     \
                        qstride, shard_cap, counts)
-    const bool small = sc.lane_stack <= kLaneStackSmall;
-    if (sc.n_bez > 0) { if (small) RT_EXTEND(kLaneStackSmall, true); else RT_EXTEND(kLaneStack, true); }
-    else { if (small) RT_EXTEND(kLaneStackSmall, false); else RT_EXTEND(kLaneStack, false); }
+#define RT_EXTEND_F(F) do { if (sc.lane_stack <= kLaneStackSmall) RT_EXTEND(kLaneStackSmall, F); else RT_EXTEND(kLaneStack, F); } while (0)
+    switch (scene_features(sc)) {
+    case 0: RT_EXTEND_F(0); break;
+    case 1: RT_EXTEND_F(1); break;
+    case 2: RT_EXTEND_F(2); break;
+    default: RT_EXTEND_F(3); break;
+    }
+#undef RT_EXTEND_F
 #undef RT_EXTEND
     return hipGetLastError();
 }
@@ -1099,11 +1202,16 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, unsigned long long* seg_count, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-#define RT_FINISH(LS, BEZ) \
-    hipLaunchKernelGGL((k_finish<LS, BEZ>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count)
-    const bool small = sc.lane_stack <= kLaneStackSmall;
-    if (sc.n_bez > 0) { if (small) RT_FINISH(kLaneStackSmall, true); else RT_FINISH(kLaneStack, true); }
-    else { if (small) RT_FINISH(kLaneStackSmall, false); else RT_FINISH(kLaneStack, false); }
+#define RT_FINISH(LS, F) \
+    hipLaunchKernelGGL((k_finish<LS, F>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count)
+#define RT_FINISH_F(F) do { if (sc.lane_stack <= kLaneStackSmall) RT_FINISH(kLaneStackSmall, F); else RT_FINISH(kLaneStack, F); } while (0)
+    switch (scene_features(sc)) {
+    case 0: RT_FINISH_F(0); break;
+    case 1: RT_FINISH_F(1); break;
+    case 2: RT_FINISH_F(2); break;
+    default: RT_FINISH_F(3); break;
+    }
+#undef RT_FINISH_F
 #undef RT_FINISH
     return hipGetLastError();
 }

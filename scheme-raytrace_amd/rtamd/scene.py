@@ -152,6 +152,17 @@ def bezier_array(cps, width, material):
     return Hitable("curves", arr, float(width), material)
 
 
+def make_constant_medium(obj, density, a):
+    """g:make-constant-medium (geometry.scm:545-578): a participating medium
+    of the given density inside ``obj`` whose phase function is
+    (m:make-lambertian a).  Its hit test draws a random number."""
+    _need(obj, Hitable, "make-constant-medium boundary")
+    _need(a, Texture, "make-constant-medium albedo")
+    if not float(density) > 0.0:
+        raise ValueError("make-constant-medium: density must be positive")
+    return Hitable("medium", obj, float(density), a)
+
+
 def flip_normals(obj):
     """g:flip-normals (geometry.scm:433-442)."""
     _need(obj, Hitable, "flip-normals")
@@ -314,6 +325,8 @@ def emit(scene, b):
         elif o.kind == "curves":
             first = b.bezier_array(a[0], a[1], mat(a[2]))
             r = b.list(list(range(first, first + a[0].shape[0])))
+        elif o.kind == "medium":
+            r = b.constant_medium(obj(a[0]), a[1], tex(a[2]))
         elif o.kind == "flip":
             r = b.flip_normals(obj(a[0]))
         elif o.kind == "box":

@@ -194,6 +194,28 @@ def cornell_bezier(nx, ny):
     return g.make_scene(objs, cornell_camera_for(nx, ny), g.sky_color)
 
 
+def cornell_smoke(nx, ny):
+    """cornell-smoke (main.scm:375-398): the Cornell boxes as constant media
+    of density 0.01 (white and black smoke), a larger light, black sky."""
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    green = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.45, 0.15)))
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(3, 3, 3)))
+    b1 = g.translate(g.rotate_y(g.make_box(v.vec3(0, 0, 0), v.vec3(165, 165, 165), white), -18), v.vec3(130, 0, 65))
+    b2 = g.translate(g.rotate_y(g.make_box(v.vec3(0, 0, 0), v.vec3(165, 330, 165), white), 15), v.vec3(265, 0, 295))
+    objs = [
+        g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, green)),
+        g.make_yz_rect(0, 555, 0, 555, 0, red),
+        g.flip_normals(g.make_xz_rect(113, 443, 127, 432, 554, light)),
+        g.flip_normals(g.make_xz_rect(0, 555, 0, 555, 555, white)),
+        g.make_xz_rect(0, 555, 0, 555, 0, white),
+        g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white)),
+        g.make_constant_medium(b1, 0.01, g.constant_texture(v.vec3(1, 1, 1))),
+        g.make_constant_medium(b2, 0.01, g.constant_texture(v.vec3(0, 0, 0))),
+    ]
+    return g.make_scene(objs, cornell_camera_for(nx, ny), g.black)
+
+
 CURVE_SEED = 0x5EED0005
 
 
@@ -251,6 +273,7 @@ SCENES = {
     "bvh_sah": test_scene_bvh_sah,
     "test_bezier": test_bezier,
     "cornell_bezier": cornell_bezier,
+    "cornell_smoke": cornell_smoke,
     "curves": cornell_curves,
     "curves_small": cornell_curves_small,
 }

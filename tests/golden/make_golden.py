@@ -277,10 +277,13 @@ SCENE_EXPR = {
     # Cornell frame with one wide curve
     "test_bezier": ("define", "test-bezier"),
     "cornell_bezier": ("define", "cornell-bezier"),
+    # participating media: make-constant-medium draws inside its hit test
+    "cornell_smoke": ("define", "cornell-smoke"),
 }
 
 SIZES = {"test_scene": (24, 16, 3), "test_scene2": (24, 16, 3), "cornell": (16, 16, 6), "cover": (24, 12, 2),
-         "bvh_sah": (24, 12, 2), "test_bezier": (32, 18, 2), "cornell_bezier": (16, 16, 4)}
+         "bvh_sah": (24, 12, 2), "test_bezier": (32, 18, 2), "cornell_bezier": (16, 16, 4),
+         "cornell_smoke": (16, 16, 4)}
 
 
 def render(ref, name):

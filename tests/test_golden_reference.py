@@ -20,7 +20,8 @@ from rtamd import perlin, scenes
 from rtamd.camera import make_camera
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-SCENES = ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier", "cornell_bezier"]
+SCENES = ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier", "cornell_bezier",
+          "cornell_smoke"]
 
 
 def F(x):

@@ -47,6 +47,7 @@ def _both(scene, nx, ny, spp, oracle_mod, spp_begin=0, seed=SEED):
     ("test_bezier", 64, 36, 4),
     ("cornell_bezier", 48, 48, 8),
     ("curves_small", 64, 36, 2),
+    ("cornell_smoke", 48, 48, 8),
 ])
 def test_scene_parity(name, nx, ny, spp, gpu_ctx, oracle_mod):
     scene = scenes.SCENES[name](nx, ny)
@@ -193,7 +194,7 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier",
-                                  "cornell_bezier"])
+                                  "cornell_bezier", "cornell_smoke"])
 def test_gpu_vs_reference_fixtures(name, gpu_ctx):
     """The GPU against the outputs of the REFERENCE's own source, executed
     (tests/golden/make_golden.py): same scene, seed and streams."""
@@ -242,3 +243,29 @@ def test_curves_c5_scale(gpu_ctx, oracle_mod):
     o.render_pixels(nx, ny, 0, 1, SEED, ref, pix, nthreads=os.cpu_count() or 1)
     for j in pix:
         assert np.abs(acc[3 * j:3 * j + 3] - ref[3 * j:3 * j + 3]).max() <= 1e-9, j
+
+
+def test_media_in_list_order(gpu_ctx, oracle_mod):
+    """A medium listed between other objects (and a sphere-bounded one, and
+    one under an instance) draws its random number with the closest hit of
+    the objects before it only: GPU vs oracle."""
+    from rtamd import scene as g
+    from rtamd.camera import make_camera
+    white = g.make_lambertian(g.constant_texture((0.73, 0.73, 0.73)))
+    red = g.make_lambertian(g.constant_texture((0.65, 0.05, 0.05)))
+    light = g.make_diffuse_light(g.constant_texture((4, 4, 4)))
+    objs = [
+        g.make_sphere((0, -1000, 0), 1000, white),
+        g.make_constant_medium(g.make_sphere((0, 1, 0), 1, white), 0.8, g.constant_texture((0.2, 0.4, 0.9))),
+        g.make_sphere((1.2, 0.7, 0.5), 0.7, red),
+        g.translate(g.rotate_y(g.make_constant_medium(g.make_box((0, 0, 0), (1, 1, 1), white), 1.5,
+                                                      g.constant_texture((0.9, 0.9, 0.9))), 30), (-2, 0, 0)),
+        g.make_xz_rect(-3, 3, -3, 3, 5, light),
+    ]
+    sc = g.make_scene(objs, make_camera((0, 2, 6), (0, 0.5, 0), (0, 1, 0), 50, 1.5, 0, 1, 0, 1), g.sky_color)
+    nx, ny, spp = 60, 40, 8
+    acc, ref = _both(sc, nx, ny, spp, oracle_mod)
+    rms, dmax, nbad, npx = _compare(acc, ref, spp)
+    print("media order: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)

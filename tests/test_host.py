@@ -154,3 +154,19 @@ def test_ppm_writer_flips_rows(tmp_path):
     assert lines[0] == "P3" and lines[1] == " 2 3" and lines[2] == "255"   # main.scm:442
     assert lines[3] == "12 13 14"                     # top row first = y = ny-1 (main.scm:445)
     assert lines[-1] == "3 4 5"
+
+
+def test_medium_order_segments():
+    """Media split the object list: a constant medium listed before other
+    objects is committed without error and keeps its list position (the
+    GPU-side order is checked against the oracle in test_gpu_parity)."""
+    from rtamd import scene as g
+    from rtamd.camera import make_camera
+    white = g.make_lambertian(g.constant_texture((0.73, 0.73, 0.73)))
+    box = g.make_box((0, 0, 0), (1, 1, 1), white)
+    sc = g.make_scene([g.make_constant_medium(box, 0.5, g.constant_texture((1, 1, 1))),
+                       g.make_sphere((0, 0, -3), 1, white)],
+                      make_camera((0, 0, 3), (0, 0, 0), (0, 1, 0), 40, 1, 0, 1, 0, 1), g.sky_color)
+    assert [o.kind for o in sc.obj_list] == ["medium", "sphere"]
+    with pytest.raises(ValueError):
+        g.make_constant_medium(box, 0.0, g.constant_texture((1, 1, 1)))
