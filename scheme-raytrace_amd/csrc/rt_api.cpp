@@ -490,26 +490,31 @@ int commit_scene(Scene* s, int world) {
     std::vector<MediumRec> med;
     std::vector<LeafInfo> lmed;
     std::vector<Group> bgroups;
-    // records of one leaf (boundary leaves get no LeafInfo: they are never a closest hit)
-    auto add_record = [&](const LeafTmp& L, LeafInfo* li) {
+    // records of one leaf.  Leaf id = leaf_base[type] + index in the type's
+    // record array, so every record gets a LeafInfo; boundary leaves (never a
+    // closest hit) get a placeholder.
+    auto add_record = [&](const LeafTmp& L, LeafInfo* li_world) {
         const Obj& o = s->objs[L.obj];
+        LeafInfo placeholder{};
+        placeholder.type = L.type; placeholder.group = -1; placeholder.mat = 0;
+        LeafInfo* li = li_world ? li_world : &placeholder;
         if (L.type == LEAF_SPHERE) {
-            if (li) { li->local = (int)sph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lsph.push_back(*li); }
+            li->local = (int)sph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lsph.push_back(*li);
             sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
         } else if (L.type == LEAF_MSPHERE) {
             MSphereRec m{};
             m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
             m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
             m.t0 = o.t0; m.den = o.t1 - o.t0;
-            if (li) { li->local = (int)msph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lmsph.push_back(*li); }
+            li->local = (int)msph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lmsph.push_back(*li);
             msph.push_back(m);
         } else if (L.type == LEAF_BEZIER) {
-            if (li) { li->local = (int)bez.size(); lbez.push_back(*li); }
+            li->local = (int)bez.size(); lbez.push_back(*li);
             bez.push_back(bezier_rec(o));
         } else {
             RectRec r{};
             r.a0 = o.a0; r.a1 = o.a1; r.b0 = o.b0; r.b1 = o.b1; r.k = o.k;
-            if (li) { li->local = (int)rect.size(); lrect[L.type - LEAF_RECT_XY].push_back(*li); }
+            li->local = (int)rect.size(); lrect[L.type - LEAF_RECT_XY].push_back(*li);
             rect.push_back(r);
         }
     };
@@ -566,6 +571,9 @@ int commit_scene(Scene* s, int world) {
         med.push_back(m);
         lmed.push_back(li);
     }
+    if (lsph.size() != sph.size() || lmsph.size() != msph.size() || lbez.size() != bez.size() ||
+        lrect[0].size() + lrect[1].size() + lrect[2].size() != rect.size())
+        return fail("internal: leaf records and leaf infos out of step");
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
     std::vector<LeafInfo> leaves;
     int32_t base[kLeafTypes];
