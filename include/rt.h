@@ -90,6 +90,8 @@ int rt_add_flip_normals(int scene, int obj, int* out_obj);                      
  * texture albedo_tex, created by this call.  Its hit test draws one random number (like the reference),
  * so media are evaluated in object-list order relative to the objects before them. */
 int rt_add_constant_medium(int scene, int boundary, double density, int albedo_tex, int* out_obj);
+/* g:make-klein center mat (geometry.scm:645): Kleinian limit set, sphere traced (no bounding box) */
+int rt_add_klein(int scene, const double center[3], int mat, int* out_obj);
 int rt_add_box(int scene, const double p0[3], const double p1[3], int mat, int* out_obj);       /* g:make-box :444 */
 int rt_add_translate(int scene, int obj, const double offset[3], int* out_obj);                 /* g:translate :465 */
 int rt_add_rotate_y(int scene, int obj, double angle_deg, int* out_obj);                        /* g:rotate-y :483 */

@@ -49,6 +49,7 @@ def lib():
             "orc_add_flip_normals": ([V, ctypes.c_int], ctypes.c_int),
             "orc_add_bezier": ([V, _dp, ctypes.c_double, ctypes.c_int], ctypes.c_int),
             "orc_add_constant_medium": ([V, ctypes.c_int, ctypes.c_double, ctypes.c_int], ctypes.c_int),
+            "orc_add_klein": ([V, _dp, ctypes.c_int], ctypes.c_int),
             "orc_add_bezier_array": ([V, _dp, ctypes.c_int, ctypes.c_double, ctypes.c_int], ctypes.c_int),
             "orc_add_box": ([V, _dp, _dp, ctypes.c_int], ctypes.c_int),
             "orc_add_translate": ([V, ctypes.c_int, _dp], ctypes.c_int),
@@ -144,6 +145,9 @@ class OracleScene:
 
     def flip_normals(self, o):
         return self.L.orc_add_flip_normals(self.s, o)
+
+    def klein(self, center, mat):
+        return self.L.orc_add_klein(self.s, _dv(center), mat)
 
     def constant_medium(self, boundary, density, tex):
         return self.L.orc_add_constant_medium(self.s, boundary, density, tex)

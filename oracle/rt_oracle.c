@@ -112,7 +112,7 @@ static inline v3 point_at(ray_t r, double t) { return vadd(r.o, vscale(r.d, t));
 enum { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum { OBJ_SPHERE = 0, OBJ_MOVING_SPHERE, OBJ_RECT, OBJ_FLIP, OBJ_BOX, OBJ_TRANSLATE,
-       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH, OBJ_BEZIER, OBJ_MEDIUM };
+       OBJ_ROTATE_Y, OBJ_LIST, OBJ_BVH, OBJ_BEZIER, OBJ_MEDIUM, OBJ_KLEIN };
 
 typedef struct { int type, a, b; v3 rgb; double scale; } orc_tex;
 typedef struct { int type, tex; double fuzz, ref_idx; } orc_mat;
@@ -266,6 +266,12 @@ int orc_add_bezier(orc_scene* s, const double* cps, double width, int mat) {
     int i = new_obj(s, OBJ_BEZIER);
     for (int k = 0; k < 4; ++k) s->obj[i].cp[k] = V(cps[3 * k], cps[3 * k + 1], cps[3 * k + 2]);
     s->obj[i].width = width; s->obj[i].mat = mat;
+    return i;
+}
+
+int orc_add_klein(orc_scene* s, const double c[3], int mat) {
+    int i = new_obj(s, OBJ_KLEIN);
+    s->obj[i].c0 = V(c[0], c[1], c[2]); s->obj[i].mat = mat;
     return i;
 }
 
@@ -565,6 +571,52 @@ static int bezier_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitre
 
 static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec);
 
+/* ---------------------------------------- Kleinian limit set, geometry.scm:590-664 */
+static const double KLEIN_SP[6][3] = {{300, 300, 0}, {300, -300, 0}, {-300, 300, 0},
+                                      {-300, -300, 0}, {0, 0, 424.26}, {0, 0, -424.26}};
+/* dist-func :609-635: sphere inversions (at most 10), then a scaled sphere distance */
+static double klein_dist(v3 center, v3 p) {
+    v3 pos = vsub(p, center);
+    double dr = 1;
+    for (int iter = 0;; ++iter) {
+        if (iter >= 10) return 0.7 * ((vlength(pos) - 125) / fabs(dr));
+        int idx = 0;
+        for (; idx < 6; ++idx)
+            if (vlength(vsub(pos, V(KLEIN_SP[idx][0], KLEIN_SP[idx][1], KLEIN_SP[idx][2]))) < 300) break;
+        if (idx == 6) return 0.7 * ((vlength(pos) - 125) / fabs(dr));
+        v3 sp = V(KLEIN_SP[idx][0], KLEIN_SP[idx][1], KLEIN_SP[idx][2]);
+        v3 diff = vsub(pos, sp);
+        dr = dr * (90000 / vdot(diff, diff));
+        double l = vlength(diff);
+        pos = vadd(vscale(vscale(diff, 90000), 1 / (l * l)), sp);
+    }
+}
+/* get-normal :637-643 */
+static v3 klein_normal(v3 center, v3 p) {
+    return vunit(V(klein_dist(center, vadd(p, V(0.01, 0, 0))) - klein_dist(center, vsub(p, V(0.01, 0, 0))),
+                   klein_dist(center, vadd(p, V(0, 0.01, 0))) - klein_dist(center, vsub(p, V(0, 0.01, 0))),
+                   klein_dist(center, vadd(p, V(0, 0, 0.01))) - klein_dist(center, vsub(p, V(0, 0, 0.01)))));
+}
+/* make-klein's hit :655-670: sphere tracing with the raw direction */
+static int klein_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitrec* rec) {
+    double len = 0;
+    v3 pos = r.o;
+    for (int iter = 0; iter < 100; ++iter) {
+        double dist = klein_dist(o->c0, pos);
+        len = len + dist;
+        pos = vadd(r.o, vscale(r.d, len));
+        if (dist < 0.001 && tmin < len && len < tmax) {
+            rec->t = len;
+            rec->p = point_at(r, len);
+            rec->n = klein_normal(o->c0, pos);
+            rec->mat = o->mat;
+            rec->u = 0; rec->v = 0;
+            return 1;
+        }
+    }
+    return 0;
+}
+
 /* The path's random stream, for hit functions that draw (the constant
  * medium, geometry.scm:564): set by color() around each world hit. */
 static __thread orc_rng* tl_rng;
@@ -664,6 +716,8 @@ static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax
         return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
     case OBJ_BEZIER:
         return bezier_hit(o, r, tmin, tmax, rec);
+    case OBJ_KLEIN:
+        return klein_hit(o, r, tmin, tmax, rec);
     case OBJ_MEDIUM: {                                                  /* :545-578 */
         hitrec r1, r2;
         if (!hit_obj(s, o->child, r, -ORC_TMAX, ORC_TMAX, &r1)) return 0;

@@ -45,7 +45,7 @@ int fail(const std::string& msg) { g_err = msg; return 1; }
     } while (0)
 
 // ------------------------------------------------------------- objects
-enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH, O_BEZIER, O_MEDIUM };
+enum ObjType { O_SPHERE, O_MSPHERE, O_RECT, O_FLIP, O_BOX, O_TRANSLATE, O_ROTATE_Y, O_LIST, O_BVH, O_BEZIER, O_MEDIUM, O_KLEIN };
 
 struct Obj {
     ObjType type;
@@ -94,7 +94,7 @@ struct Scene {
 
     // flattened + uploaded
     DevScene dev{};
-    DevBuf d_sph, d_msph, d_rect, d_bez, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
+    DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     // render buffers
     DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
     uint32_t* h_counts = nullptr;     // pinned
@@ -182,6 +182,10 @@ struct Flattener {
         case O_BEZIER:
             if (in_boundary) return fail("a constant medium's boundary may hold spheres, rects, boxes and instances only");
             leaves.push_back({LEAF_BEZIER, chain_id(), flip, id});
+            break;
+        case O_KLEIN:
+            if (in_boundary) return fail("a constant medium's boundary may hold spheres, rects, boxes and instances only");
+            leaves.push_back({LEAF_KLEIN, chain_id(), flip, id});
             break;
         case O_MEDIUM: {
             if (in_boundary) return fail("constant media cannot be nested");
@@ -355,6 +359,8 @@ int commit_scene(Scene* s, int world) {
 
     std::vector<BezierRec> bez;
     std::vector<LeafInfo> lbez;
+    std::vector<KleinRec> klein;
+    std::vector<LeafInfo> lklein;
     auto bezier_rec = [](const Obj& o) {
         BezierRec b{};
         for (int k = 0; k < 12; ++k) b.cp[k] = o.cp[k];
@@ -511,6 +517,9 @@ int commit_scene(Scene* s, int world) {
         } else if (L.type == LEAF_BEZIER) {
             li->local = (int)bez.size(); lbez.push_back(*li);
             bez.push_back(bezier_rec(o));
+        } else if (L.type == LEAF_KLEIN) {
+            li->local = (int)klein.size(); lklein.push_back(*li);
+            klein.push_back({o.c0[0], o.c0[1], o.c0[2], 0.0});
         } else {
             RectRec r{};
             r.a0 = o.a0; r.a1 = o.a1; r.b0 = o.b0; r.b1 = o.b1; r.k = o.k;
@@ -520,12 +529,13 @@ int commit_scene(Scene* s, int world) {
     };
     auto type_size = [&](int type) {
         return (type == LEAF_SPHERE) ? sph.size() : (type == LEAF_MSPHERE) ? msph.size()
-             : (type == LEAF_BEZIER) ? bez.size() : rect.size();
+             : (type == LEAF_BEZIER) ? bez.size() : (type == LEAF_KLEIN) ? klein.size() : rect.size();
     };
     // group a leaf subset by (chain, type) into `out`; world leaves also get LeafInfo
     auto emit_groups = [&](const std::vector<const LeafTmp*>& ls, std::vector<Group>& out, bool world, bool skip_bvh) {
         for (int ch : chain_order) {
-            for (int type = LEAF_SPHERE; type <= LEAF_BEZIER; ++type) {
+            for (int type = LEAF_SPHERE; type <= LEAF_KLEIN; ++type) {
+                if (type == LEAF_MEDIUM) continue;
                 if (skip_bvh && ch == -1 && (type == LEAF_SPHERE || type == LEAF_MSPHERE || type == LEAF_BEZIER)) continue;
                 Group g{type, ch, 0, 0};
                 const size_t before = type_size(type);
@@ -572,6 +582,7 @@ int commit_scene(Scene* s, int world) {
         lmed.push_back(li);
     }
     if (lsph.size() != sph.size() || lmsph.size() != msph.size() || lbez.size() != bez.size() ||
+        lklein.size() != klein.size() ||
         lrect[0].size() + lrect[1].size() + lrect[2].size() != rect.size())
         return fail("internal: leaf records and leaf infos out of step");
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
@@ -591,6 +602,8 @@ int commit_scene(Scene* s, int world) {
     for (auto& li : lbez) leaves.push_back(li);
     base[LEAF_MEDIUM] = (int32_t)leaves.size();
     for (auto& li : lmed) leaves.push_back(li);
+    base[LEAF_KLEIN] = (int32_t)leaves.size();
+    for (auto& li : lklein) leaves.push_back(li);
 
     std::vector<Chain> chains;
     for (auto& cv : f.chains) {
@@ -607,6 +620,8 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_groups, groups, &d.groups)) return rc;
     if (int rc = upload(s->d_bez, bez, &d.bez)) return rc;
     d.n_bez = (int)bez.size();
+    if (int rc = upload(s->d_klein, klein, &d.klein)) return rc;
+    d.n_klein = (int)klein.size();
     if (int rc = upload(s->d_med, med, &d.med)) return rc;
     d.n_med = (int)med.size();
     if (int rc = upload(s->d_bgroups, bgroups, &d.bgroups)) return rc;
@@ -988,6 +1003,15 @@ int rt_add_bezier_array(int scene, const double* cps, int n, double width, int m
         s->objs.push_back(std::move(o));
     }
     return 0;
+}
+int rt_add_klein(int scene, const double center[3], int mat, int* out) {
+    SCENE_OR_FAIL(s, scene);
+    OUT_OR_FAIL(out);
+    if (!center) return fail("rt_add_klein: null centre");
+    if (check_mat(s, mat)) return 1;
+    Obj o; o.type = O_KLEIN; o.mat = mat;
+    for (int k = 0; k < 3; ++k) o.c0[k] = center[k];
+    return push_obj(s, std::move(o), out);
 }
 int rt_add_constant_medium(int scene, int boundary, double density, int albedo_tex, int* out) {
     SCENE_OR_FAIL(s, scene);

@@ -22,11 +22,11 @@ constexpr int kMaxChain = 4;                   // instance ops per leaf chain
 enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum LeafType : int32_t { LEAF_SPHERE = 0, LEAF_MSPHERE = 1, LEAF_RECT_XY = 2, LEAF_RECT_XZ = 3,
-                          LEAF_RECT_YZ = 4, LEAF_BEZIER = 5, LEAF_MEDIUM = 6 };
-constexpr int kLeafTypes = 7;
-constexpr int32_t GROUP_BVH = 7;               // group type: BVH over world-level spheres / curves
-// closest-hit kernel variants: scene features compiled in
-constexpr int kFeatCurves = 1, kFeatMedia = 2;
+                          LEAF_RECT_YZ = 4, LEAF_BEZIER = 5, LEAF_MEDIUM = 6, LEAF_KLEIN = 7 };
+constexpr int kLeafTypes = 8;
+constexpr int32_t GROUP_BVH = 8;               // group type: BVH over world-level spheres / curves
+// closest-hit kernel variants: scene features compiled in (extra = constant media, Klein limit sets)
+constexpr int kFeatCurves = 1, kFeatExtra = 2;
 enum ChainOp : int32_t { OP_TRANSLATE = 0, OP_ROTATE_Y = 1 };
 
 struct DevTexture {            // texture.scm:12-34
@@ -53,6 +53,9 @@ constexpr int kBezMaxDepth = 24;               // subdivision levels the curve t
 // Constant medium (geometry.scm:545-578): its boundary is the closest hit over
 // the boundary groups [bg_begin, bg_end) of DevScene::bgroups; neg_inv_density
 // = (- (/ 1 density)).  The phase function is a lambertian material.
+// Kleinian limit set (geometry.scm:590-673): its centre; the six inversion
+// spheres and radii are the module's constants.
+struct alignas(32) KleinRec { double cx, cy, cz, pad; };
 struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density, pad; };
 
 // BVH over the world-level spheres, moving spheres and curves, per-lane
@@ -92,6 +95,7 @@ struct DevScene {
     const RectRec* rect;   int32_t n_rect;
     const BezierRec* bez;  int32_t n_bez;
     const MediumRec* med;  int32_t n_med;
+    const KleinRec* klein; int32_t n_klein;
     const Group* bgroups;  int32_t n_bgroups;     // medium boundaries (not part of the world loop)
     const Group* groups;   int32_t n_groups;
     const BvhNode2* bvh2;  int32_t n_bvh2;

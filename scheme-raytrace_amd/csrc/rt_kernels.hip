@@ -585,6 +585,51 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
 // (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
 // walks the same group / primitive sequence, so the primitive records are
 // fetched once per wave through the scalar unit.
+// --------------------------------------------- Kleinian limit set (f4)
+// geometry.scm:596-673: six inversion spheres, at most 10 inversions per
+// distance estimate, sphere tracing (at most 100 steps) along the raw ray.
+__device__ __forceinline__ v3 klein_sphere(const int i) {
+    return (i == 0) ? mk(300.0, 300.0, 0.0) : (i == 1) ? mk(300.0, -300.0, 0.0)
+         : (i == 2) ? mk(-300.0, 300.0, 0.0) : (i == 3) ? mk(-300.0, -300.0, 0.0)
+         : (i == 4) ? mk(0.0, 0.0, 424.26) : mk(0.0, 0.0, -424.26);
+}
+__device__ __forceinline__ double klein_dist(const v3 center, const v3 p) {         // dist-func :609-635
+    v3 pos = p - center;
+    double dr = 1.0;
+    for (int iter = 0; iter < 10; ++iter) {
+        int idx = 0;
+        v3 sp = klein_sphere(0);
+        for (; idx < 6; ++idx) {
+            sp = klein_sphere(idx);
+            if (length(pos - sp) < 300.0) break;
+        }
+        if (idx == 6) break;
+        const v3 diff = pos - sp;
+        dr = dr * (90000.0 / dot(diff, diff));
+        const double l = length(diff);
+        pos = (diff * 90000.0) * (1.0 / (l * l)) + sp;
+    }
+    return 0.7 * ((length(pos) - 125.0) / fabs(dr));
+}
+__device__ __noinline__ v3 klein_normal(const v3 center, const v3 p) {               // get-normal :637-643
+    return unit(mk(klein_dist(center, p + mk(0.01, 0.0, 0.0)) - klein_dist(center, p - mk(0.01, 0.0, 0.0)),
+                   klein_dist(center, p + mk(0.0, 0.01, 0.0)) - klein_dist(center, p - mk(0.0, 0.01, 0.0)),
+                   klein_dist(center, p + mk(0.0, 0.0, 0.01)) - klein_dist(center, p - mk(0.0, 0.0, 0.01))));
+}
+__device__ __forceinline__ bool klein_test(const KleinRec& K, const v3 o, const v3 d, const double tmax,
+                                           double& tout) {                             // make-klein :655-670
+    const v3 c = mk(K.cx, K.cy, K.cz);
+    double len = 0.0;
+    v3 pos = o;
+    for (int iter = 0; iter < 100; ++iter) {
+        const double dist = klein_dist(c, pos);
+        len = len + dist;
+        pos = o + d * len;
+        if (dist < 0.001 && kTmin < len && len < tmax) { tout = len; return true; }
+    }
+    return false;
+}
+
 // ------------------------------------------------------- constant medium
 // Closest boundary hit in (tmin, tmax) over a medium's boundary groups, with
 // the reference's hit semantics (spheres strict, rects non-strict).
@@ -666,7 +711,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
                                                const double time, double& closest, uint32_t* lstk,
                                                const int lmax, BezWave* bw, Rng* rng) {
     constexpr bool BEZ = (F & kFeatCurves) != 0;
-    constexpr bool MED = (F & kFeatMedia) != 0;
+    constexpr bool MED = (F & kFeatExtra) != 0;
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
@@ -697,6 +742,13 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
                 }
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
+            }
+        } else if (G.type == LEAF_KLEIN) {                 // geometry.scm:645-673
+            if (MED) {
+                for (int s = G.begin; s < G.end; ++s) {
+                    double t;
+                    if (klein_test(sc.klein[s], o, d, closest, t)) { closest = t; best = base + s; }
+                }
             }
         } else if (G.type == LEAF_MEDIUM) {                // geometry.scm:545-578
             if (MED) {
@@ -836,7 +888,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     __shared__ uint32_t s_lstack[256 * LS];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
     constexpr bool BEZ = (F & kFeatCurves) != 0;
-    constexpr bool MED = (F & kFeatMedia) != 0;
+    constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     int cls = -1;
@@ -958,6 +1010,9 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         nrm = mk(0.0, 1.0, 0.0);
     } else if (li.type == LEAF_RECT_YZ || li.type == LEAF_MEDIUM) {
         nrm = mk(1.0, 0.0, 0.0);                             // medium: (v:vec3 1 0 0), geometry.scm:569
+    } else if (li.type == LEAF_KLEIN) {
+        const KleinRec K = sc.klein[li.local];
+        nrm = klein_normal(mk(K.cx, K.cy, K.cz), pt);        // at ray-pos = point-at-parameter, :664
     } else {
         nrm = d * -1.0;                                      // curve: (v:scale (dir r) -1), bezier.scm:204
     }
@@ -1094,7 +1149,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
     __shared__ PerlinLds P;
     __shared__ uint32_t s_lstack[256 * LS];
     constexpr bool BEZ = (F & kFeatCurves) != 0;
-    constexpr bool MED = (F & kFeatMedia) != 0;
+    constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
     stage_perlin(sc, P);
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
@@ -1156,7 +1211,7 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     return hipGetLastError();
 }
 static int scene_features(const DevScene& sc) {
-    return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 ? kFeatMedia : 0);
+    return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
 }
 hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,

@@ -64,6 +64,7 @@ _SIGNATURES = {
     "rt_add_bezier_array": [ctypes.c_int, _c_double_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_int_p],
     "rt_add_flip_normals": [ctypes.c_int, ctypes.c_int, _c_int_p],
     "rt_add_constant_medium": [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_int_p],
+    "rt_add_klein": [ctypes.c_int, _c_double_p, ctypes.c_int, _c_int_p],
     "rt_add_box": [ctypes.c_int, _c_double_p, _c_double_p, ctypes.c_int, _c_int_p],
     "rt_add_translate": [ctypes.c_int, ctypes.c_int, _c_double_p, _c_int_p],
     "rt_add_rotate_y": [ctypes.c_int, ctypes.c_int, ctypes.c_double, _c_int_p],

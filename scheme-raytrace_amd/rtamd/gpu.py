@@ -99,6 +99,9 @@ class GpuBuilder:
         ptr = cps.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
         return self._out("rt_add_bezier_array", ptr, int(cps.shape[0]), width, mat)
 
+    def klein(self, center, mat):
+        return self._out("rt_add_klein", dvec(center), mat)
+
     def constant_medium(self, boundary, density, tex):
         return self._out("rt_add_constant_medium", boundary, density, tex)
 

@@ -152,6 +152,15 @@ def bezier_array(cps, width, material):
     return Hitable("curves", arr, float(width), material)
 
 
+def make_klein(center, material):
+    """g:make-klein (geometry.scm:645-673): a Kleinian limit set (six
+    inversion spheres, geometry.scm:596-605) rendered by sphere tracing with
+    the raw ray direction.  It has no bounding box, so it is never put in a
+    BVH."""
+    _need(material, Material, "make-klein material")
+    return Hitable("klein", v.vec3(*center), material)
+
+
 def make_constant_medium(obj, density, a):
     """g:make-constant-medium (geometry.scm:545-578): a participating medium
     of the given density inside ``obj`` whose phase function is
@@ -325,6 +334,8 @@ def emit(scene, b):
         elif o.kind == "curves":
             first = b.bezier_array(a[0], a[1], mat(a[2]))
             r = b.list(list(range(first, first + a[0].shape[0])))
+        elif o.kind == "klein":
+            r = b.klein(a[0], mat(a[1]))
         elif o.kind == "medium":
             r = b.constant_medium(obj(a[0]), a[1], tex(a[2]))
         elif o.kind == "flip":

@@ -216,6 +216,33 @@ def cornell_smoke(nx, ny):
     return g.make_scene(objs, cornell_camera_for(nx, ny), g.black)
 
 
+def klein_scene(nx, ny):
+    """klein-scene (main.scm:400-407): ground sphere and a Kleinian limit set."""
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    objs = [g.make_sphere(v.vec3(0, -1003, -1), 1000, white), g.make_klein(v.vec3(0, 2, 0), red)]
+    return g.make_scene(objs, camera_for(nx, ny), g.sky_color)
+
+
+def cornell_klein(nx, ny):
+    """cornell-klein (main.scm:409-426): the limit set inside the Cornell frame."""
+    blue = g.make_lambertian(g.constant_texture(v.vec3(0.05, 0.65, 0.65)))
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    green = g.make_lambertian(g.constant_texture(v.vec3(0.12, 0.45, 0.15)))
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(3, 3, 3)))
+    objs = [
+        g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, green)),
+        g.make_yz_rect(0, 555, 0, 555, 0, red),
+        g.flip_normals(g.make_xz_rect(113, 443, 127, 432, 554, light)),
+        g.flip_normals(g.make_xz_rect(0, 555, 0, 555, 555, white)),
+        g.make_xz_rect(0, 555, 0, 555, 0, white),
+        g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white)),
+        g.make_klein(v.vec3(250, 200, 280), blue),
+    ]
+    return g.make_scene(objs, cornell_camera_for(nx, ny), g.sky_color)
+
+
 CURVE_SEED = 0x5EED0005
 
 
@@ -274,6 +301,8 @@ SCENES = {
     "test_bezier": test_bezier,
     "cornell_bezier": cornell_bezier,
     "cornell_smoke": cornell_smoke,
+    "klein": klein_scene,
+    "cornell_klein": cornell_klein,
     "curves": cornell_curves,
     "curves_small": cornell_curves_small,
 }

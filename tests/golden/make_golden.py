@@ -279,11 +279,14 @@ SCENE_EXPR = {
     "cornell_bezier": ("define", "cornell-bezier"),
     # participating media: make-constant-medium draws inside its hit test
     "cornell_smoke": ("define", "cornell-smoke"),
+    # Kleinian limit set, sphere traced (geometry.scm:590-673)
+    "klein": ("define", "klein-scene"),
+    "cornell_klein": ("define", "cornell-klein"),
 }
 
 SIZES = {"test_scene": (24, 16, 3), "test_scene2": (24, 16, 3), "cornell": (16, 16, 6), "cover": (24, 12, 2),
          "bvh_sah": (24, 12, 2), "test_bezier": (32, 18, 2), "cornell_bezier": (16, 16, 4),
-         "cornell_smoke": (16, 16, 4)}
+         "cornell_smoke": (16, 16, 4), "klein": (24, 16, 2), "cornell_klein": (16, 16, 2)}
 
 
 def render(ref, name):

@@ -1317,17 +1317,26 @@ class Interp:
         return run
 
 
+def _one(v):
+    """A multiple-values result in a single-value context: Gauche takes the
+    first value (e.g. get-normal subtracting dist-func results,
+    geometry.scm:637-643)."""
+    if v.__class__ is Values:
+        return v[0] if len(v) else UNDEF
+    return v
+
+
 def _make_call(fc, acs):
     n = len(acs)
     if n == 0:
         return lambda env: fc(env)()
     if n == 1:
         a0 = acs[0]
-        return lambda env: fc(env)(a0(env))
+        return lambda env: fc(env)(_one(a0(env)))
     if n == 2:
         a0, a1 = acs
-        return lambda env: fc(env)(a0(env), a1(env))
+        return lambda env: fc(env)(_one(a0(env)), _one(a1(env)))
     if n == 3:
         a0, a1, a2 = acs
-        return lambda env: fc(env)(a0(env), a1(env), a2(env))
-    return lambda env: fc(env)(*[a(env) for a in acs])
+        return lambda env: fc(env)(_one(a0(env)), _one(a1(env)), _one(a2(env)))
+    return lambda env: fc(env)(*[_one(a(env)) for a in acs])

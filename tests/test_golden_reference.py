@@ -21,7 +21,7 @@ from rtamd.camera import make_camera
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SCENES = ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier", "cornell_bezier",
-          "cornell_smoke"]
+          "cornell_smoke", "klein", "cornell_klein"]
 
 
 def F(x):

@@ -48,6 +48,7 @@ def _both(scene, nx, ny, spp, oracle_mod, spp_begin=0, seed=SEED):
     ("cornell_bezier", 48, 48, 8),
     ("curves_small", 64, 36, 2),
     ("cornell_smoke", 48, 48, 8),
+    ("cornell_klein", 32, 32, 2),
 ])
 def test_scene_parity(name, nx, ny, spp, gpu_ctx, oracle_mod):
     scene = scenes.SCENES[name](nx, ny)
@@ -194,7 +195,7 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier",
-                                  "cornell_bezier", "cornell_smoke"])
+                                  "cornell_bezier", "cornell_smoke", "klein", "cornell_klein"])
 def test_gpu_vs_reference_fixtures(name, gpu_ctx):
     """The GPU against the outputs of the REFERENCE's own source, executed
     (tests/golden/make_golden.py): same scene, seed and streams."""
