@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -315,6 +316,18 @@ struct BvhBuild {
     }
 };
 
+// f64 -> f32 rounded toward -inf / +inf (BVH boxes stay conservative)
+float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+
 void pad_box(double* lo, double* hi) {
     double m = 1.0;
     for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
@@ -427,6 +440,7 @@ int commit_scene(Scene* s, int world) {
     int32_t bvh2_root = 0;
     int32_t lane_stack = 0;
     bool bvh_has_bez = false;
+    float bvh_extent = 0.0f;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         bb.build(0, (int)refs.size(), 0);
@@ -455,11 +469,14 @@ int commit_scene(Scene* s, int world) {
             const BvhNode& L = bvh_nodes[bvh_nodes[i].a];
             const BvhNode& R = bvh_nodes[bvh_nodes[i].b];
             for (int k = 0; k < 3; ++k) {
-                M.lbox[k] = L.lo[k]; M.lbox[3 + k] = L.hi[k]; M.rbox[k] = R.lo[k]; M.rbox[3 + k] = R.hi[k];
+                M.lbox[k] = f32_down(L.lo[k]); M.lbox[3 + k] = f32_up(L.hi[k]);
+                M.rbox[k] = f32_down(R.lo[k]); M.rbox[3 + k] = f32_up(R.hi[k]);
             }
             M.l = ref_of(bvh_nodes[i].a); M.r = ref_of(bvh_nodes[i].b);
         }
         bvh2_root = ref_of(0);
+        for (int k = 0; k < 3; ++k)
+            bvh_extent = std::max(bvh_extent, f32_up(std::max(std::fabs(bvh_nodes[0].lo[k]), std::fabs(bvh_nodes[0].hi[k]))));
         // stack entries a per-lane traversal can need = depth of the BVH2
         std::vector<int> depth(bvh_nodes.size(), 0);
         for (size_t i = 0; i < bvh_nodes.size(); ++i)
@@ -627,6 +644,7 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_bgroups, bgroups, &d.bgroups)) return rc;
     d.n_bgroups = (int)bgroups.size();
     d.bvh_has_bez = bvh_has_bez ? 1 : 0;
+    d.bvh_extent = bvh_extent;
     if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
     d.n_bvh2 = (int)bvh2.size();

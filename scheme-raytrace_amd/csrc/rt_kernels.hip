@@ -434,20 +434,42 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
 // Per-lane BVH traversal: every lane walks its own path through the BVH2
 // (child boxes tested at the parent, nearer child first, LDS stack with a
 // block-size stride so a wave's pushes hit 64 consecutive banks).
-__device__ __forceinline__ bool box_hit_t(const double* bx, const v3 o, const v3 inv, const double closest,
-                                          double& tnear) {
-    const double tx0 = (bx[0] - o.x) * inv.x, tx1 = (bx[3] - o.x) * inv.x;
-    const double ty0 = (bx[1] - o.y) * inv.y, ty1 = (bx[4] - o.y) * inv.y;
-    const double tz0 = (bx[2] - o.z) * inv.z, tz1 = (bx[5] - o.z) * inv.z;
-    tnear = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmax(fmin(tz0, tz1), 0.0));
-    const double tfar = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmin(fmax(tz0, tz1), closest * 1.000000001));
+// f32 slab test.  With O = fl32(o), I = fl32(1/d) and f32 arithmetic, each
+// computed slab end is within 4 ulps * (|box| + |o|) * |I| of the exact one;
+// s = (extent + |O|) * |I| * 2^-19 per axis covers that, so the widened
+// interval contains the exact slab interval of the (outward-rounded) box.
+struct BoxRay { float ox, oy, oz, ix, iy, iz, sx, sy, sz; };
+__device__ __forceinline__ float f32_up(const double x) {       // x >= 0 (a ray's t range)
+    float f = (float)x;
+    if ((double)f < x) f = __int_as_float(__float_as_int(f) + 1);
+    return f;
+}
+__device__ __forceinline__ BoxRay box_ray(const v3 o, const v3 d, const float extent) {
+    BoxRay b;
+    const double lim = 1e30;
+    b.ox = (float)o.x; b.oy = (float)o.y; b.oz = (float)o.z;
+    b.ix = (float)fmax(fmin(1.0 / d.x, lim), -lim);
+    b.iy = (float)fmax(fmin(1.0 / d.y, lim), -lim);
+    b.iz = (float)fmax(fmin(1.0 / d.z, lim), -lim);
+    const float k = 1.0f / 524288.0f;                      // 2^-19
+    b.sx = (extent + fabsf(b.ox)) * fabsf(b.ix) * k;
+    b.sy = (extent + fabsf(b.oy)) * fabsf(b.iy) * k;
+    b.sz = (extent + fabsf(b.oz)) * fabsf(b.iz) * k;
+    return b;
+}
+__device__ __forceinline__ bool box_hit_t(const float* bx, const BoxRay& r, const float tcap, float& tnear) {
+    const float tx0 = (bx[0] - r.ox) * r.ix, tx1 = (bx[3] - r.ox) * r.ix;
+    const float ty0 = (bx[1] - r.oy) * r.iy, ty1 = (bx[4] - r.oy) * r.iy;
+    const float tz0 = (bx[2] - r.oz) * r.iz, tz1 = (bx[5] - r.oz) * r.iz;
+    tnear = fmaxf(fmaxf(fminf(tx0, tx1) - r.sx, fminf(ty0, ty1) - r.sy), fmaxf(fminf(tz0, tz1) - r.sz, 0.0f));
+    const float tfar = fminf(fminf(fmaxf(tx0, tx1) + r.sx, fmaxf(ty0, ty1) + r.sy), fminf(fmaxf(tz0, tz1) + r.sz, tcap));
     return tnear <= tfar;
 }
 
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
     const double a = dot(d, d);
-    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const BoxRay br = box_ray(o, d, sc.bvh_extent);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int sp = 0;
@@ -455,9 +477,10 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
     for (;;) {
         if (node >= 0) {
             const BvhNode2 N = sc.bvh2[node];
-            double tl, tr;
-            const bool hl = box_hit_t(N.lbox, o, inv, closest, tl);
-            const bool hr = box_hit_t(N.rbox, o, inv, closest, tr);
+            const float tcap = f32_up(closest);
+            float tl, tr;
+            const bool hl = box_hit_t(N.lbox, br, tcap, tl);
+            const bool hr = box_hit_t(N.rbox, br, tcap, tr);
             if (hl && hr) {
                 const bool lfirst = tl <= tr;
                 if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
@@ -494,7 +517,7 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
                                                 BezWave& W) {
     const double a = dot(d, d);
-    const v3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    const BoxRay br = box_ray(o, d, sc.bvh_extent);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     const double tscale = fmax(1.0, 1.0 / sqrt(a));
     const uint32_t lane = threadIdx.x & 63u;
@@ -509,9 +532,10 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
         if (pb >= pe && trav) {                 // lanes with curves pending only queue them below
             if (node >= 0) {
                 const BvhNode2 N = sc.bvh2[node];
-                double tl, tr;
-                const bool hl = box_hit_t(N.lbox, o, inv, closest * tscale, tl);
-                const bool hr = box_hit_t(N.rbox, o, inv, closest * tscale, tr);
+                const float tcap = f32_up(closest * tscale);
+                float tl, tr;
+                const bool hl = box_hit_t(N.lbox, br, tcap, tl);
+                const bool hr = box_hit_t(N.rbox, br, tcap, tr);
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
                     if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
