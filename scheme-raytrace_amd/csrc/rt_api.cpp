@@ -243,7 +243,8 @@ struct BvhNode { double lo[3], hi[3]; int32_t a, b, c, d; };
 struct BvhBuild {
     std::vector<PrimRef>& refs;
     std::vector<BvhNode> nodes;
-    static constexpr int kLeafMax = 4;
+    int leaf_max = 2;                 // RTAMD_BVH_LEAF
+    double trav_cost = 0.5;           // RTAMD_BVH_CT: node visit cost relative to one primitive test
     static constexpr int kBins = 16;
 
     static double area(const double* lo, const double* hi) {
@@ -267,7 +268,7 @@ struct BvhBuild {
         double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
         for (int i = b; i < e; ++i) { grow(lo, hi, refs[i].lo, refs[i].hi); grow(clo, chi, refs[i].c, refs[i].c); }
         const int n = e - b;
-        if (n <= kLeafMax || depth >= kLaneStack - 2) return make_leaf(node, b, e, lo, hi);
+        if (n <= leaf_max || depth >= kLaneStack - 2) return make_leaf(node, b, e, lo, hi);
         int axis = 0;
         for (int k = 1; k < 3; ++k) if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
         const double ext = chi[axis] - clo[axis];
@@ -294,8 +295,8 @@ struct BvhBuild {
                 if (c < best) { best = c; best_k = k; }
             }
             const double parent = area(lo, hi);
-            const bool worth = best_k > 0 && (parent <= 0 || 0.5 + best / parent < (double)n);
-            if (!worth && n <= 2 * kLeafMax) return make_leaf(node, b, e, lo, hi);
+            const bool worth = best_k > 0 && (parent <= 0 || trav_cost + best / parent < (double)n);
+            if (!worth && n <= 2 * leaf_max) return make_leaf(node, b, e, lo, hi);
             if (best_k > 0) {
                 auto it = std::partition(refs.begin() + b, refs.begin() + e,
                                          [&](const PrimRef& r) { return bin_of(r) < best_k; });
@@ -443,6 +444,8 @@ int commit_scene(Scene* s, int world) {
     float bvh_extent = 0.0f;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
+        if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("RTAMD_BVH_CT")) bb.trav_cost = std::atof(e);
         bb.build(0, (int)refs.size(), 0);
         // leaf ranges: refs order -> sphere / moving-sphere / curve array indices
         std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0), nb(refs.size() + 1, 0);

@@ -466,31 +466,49 @@ __device__ __forceinline__ bool box_hit_t(const float* bx, const BoxRay& r, cons
     return tnear <= tfar;
 }
 
+// Leaves are postponed (Aila & Laine's speculative while-while): a lane that
+// reaches a leaf parks it and keeps traversing until every active lane of
+// the wave has a leaf parked (or has finished), then the wave tests its
+// leaves together, so the f64 sphere code runs with most lanes active.
+// Deferring a leaf only delays the shrinking of `closest`, which culls less;
+// the closest hit is unchanged.
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
+    constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d);
     const BoxRay br = box_ray(o, d, sc.bvh_extent);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int sp = 0;
-    int32_t node = sc.bvh2_root;
-    for (;;) {
-        if (node >= 0) {
-            const BvhNode2 N = sc.bvh2[node];
-            const float tcap = f32_up(closest);
-            float tl, tr;
-            const bool hl = box_hit_t(N.lbox, br, tcap, tl);
-            const bool hr = box_hit_t(N.rbox, br, tcap, tr);
-            if (hl && hr) {
-                const bool lfirst = tl <= tr;
-                if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
-                node = lfirst ? N.l : N.r;
-                continue;
+    int32_t node = sc.bvh2_root, pend = kDone;
+    while (node != kDone || pend != kDone) {
+        while (node != kDone) {
+            if (node < 0) {                                   // a leaf
+                if (pend != kDone) break;                     // one is already parked
+                pend = node;
+                node = sp ? (int32_t)lstk[--sp * stride] : kDone;
+            } else {
+                const BvhNode2 N = sc.bvh2[node];
+                const float tcap = f32_up(closest);
+                float tl, tr;
+                const bool hl = box_hit_t(N.lbox, br, tcap, tl);
+                const bool hr = box_hit_t(N.rbox, br, tcap, tr);
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                    node = lfirst ? N.l : N.r;
+                } else if (hl) {
+                    node = N.l;
+                } else if (hr) {
+                    node = N.r;
+                } else {
+                    node = sp ? (int32_t)lstk[--sp * stride] : kDone;
+                }
             }
-            if (hl) { node = N.l; continue; }
-            if (hr) { node = N.r; continue; }
-        } else {
-            const BvhLeaf L = sc.bleaf[~node];
+            if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
+        }
+        if (pend != kDone) {
+            const BvhLeaf L = sc.bleaf[~pend];
             for (int s = L.sb; s < L.sb + L.sn; ++s) {
                 const SphereRec S = sc.sph[s];
                 sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
@@ -501,10 +519,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                 sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
             }
+            pend = kDone;
         }
-        if (sp == 0) break;
-        --sp;
-        node = (int32_t)lstk[sp * stride];
     }
 }
 
