@@ -350,6 +350,43 @@ int upload(DevBuf& b, const std::vector<T>& v, const T** out) {
     return 0;
 }
 
+// An L2 bound on the world-space distance from the origin of every point a
+// ray can start from: all leaves (instance chains applied: rotations keep the
+// norm, translations add theirs), medium boundaries, the camera; x4 for the
+// off-surface points curves report (Q10) and motion extrapolation.
+double scene_radius(const Scene* s, const Flattener& f) {
+    auto n3 = [](const double* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); };
+    auto chain_len = [&](int ch) {
+        double t = 0;
+        if (ch >= 0)
+            for (const ChainOpRec& op : f.chains[ch])
+                if (op.op == OP_TRANSLATE) t += std::sqrt(op.x * op.x + op.y * op.y + op.z * op.z);
+        return t;
+    };
+    auto leaf_r = [&](const LeafTmp& L) {
+        const Obj& o = s->objs[L.obj];
+        double r = 0;
+        switch (L.type) {
+        case LEAF_SPHERE: r = n3(o.c0) + std::fabs(o.r); break;
+        case LEAF_MSPHERE: r = 2 * std::max(n3(o.c0), n3(o.c1)) + std::fabs(o.r); break;
+        case LEAF_BEZIER:
+            for (int i = 0; i < 4; ++i) r = std::max(r, n3(o.cp + 3 * i));
+            r += std::fabs(o.width);
+            break;
+        case LEAF_KLEIN: r = n3(o.c0) + 1200; break;
+        case LEAF_MEDIUM: r = 0; break;
+        default:
+            r = std::sqrt(3.0) * std::max({std::fabs(o.a0), std::fabs(o.a1), std::fabs(o.b0), std::fabs(o.b1),
+                                           std::fabs(o.k)});
+        }
+        return r + chain_len(L.chain);
+    };
+    double R = n3(s->cam + 9) + std::fabs(s->cam[21]);
+    for (const LeafTmp& L : f.leaves) R = std::max(R, leaf_r(L));
+    for (const auto& b : f.bounds) for (const LeafTmp& L : b) R = std::max(R, leaf_r(L));
+    return 4 * R + 1;
+}
+
 int commit_scene(Scene* s, int world) {
     Context* c = get_ctx(s->ctx);
     if (!c) return fail("scene's context was destroyed");
@@ -441,7 +478,7 @@ int commit_scene(Scene* s, int world) {
     int32_t bvh2_root = 0;
     int32_t lane_stack = 0;
     bool bvh_has_bez = false;
-    float bvh_extent = 0.0f;
+    float bvh_pad = 0.0f;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
@@ -466,20 +503,25 @@ int commit_scene(Scene* s, int world) {
             bleaf.push_back({ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0});
         }
         auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
+        // f32 box margin: 2^-21 x a radius bound R on everything a ray can start
+        // from (x4 included, see scene_radius).  The slab ends carry at most
+        // ~4 ulps x (|box| + |o|) <= 2^-22 x 1.25 R of rounding; the margin is
+        // 1.6x that.
+        const double margin = std::ldexp(scene_radius(s, f), -21);
+        bvh_pad = (float)margin;
         for (size_t i = 0; i < bvh_nodes.size(); ++i) {
             if (inner_idx[i] < 0) continue;
             BvhNode2& M = bvh2[inner_idx[i]];
             const BvhNode& L = bvh_nodes[bvh_nodes[i].a];
             const BvhNode& R = bvh_nodes[bvh_nodes[i].b];
             for (int k = 0; k < 3; ++k) {
-                M.lbox[k] = f32_down(L.lo[k]); M.lbox[3 + k] = f32_up(L.hi[k]);
-                M.rbox[k] = f32_down(R.lo[k]); M.rbox[3 + k] = f32_up(R.hi[k]);
+                M.lbox[k] = f32_down(L.lo[k] - margin); M.lbox[3 + k] = f32_up(L.hi[k] + margin);
+                M.rbox[k] = f32_down(R.lo[k] - margin); M.rbox[3 + k] = f32_up(R.hi[k] + margin);
             }
             M.l = ref_of(bvh_nodes[i].a); M.r = ref_of(bvh_nodes[i].b);
         }
         bvh2_root = ref_of(0);
-        for (int k = 0; k < 3; ++k)
-            bvh_extent = std::max(bvh_extent, f32_up(std::max(std::fabs(bvh_nodes[0].lo[k]), std::fabs(bvh_nodes[0].hi[k]))));
+
         // stack entries a per-lane traversal can need = depth of the BVH2
         std::vector<int> depth(bvh_nodes.size(), 0);
         for (size_t i = 0; i < bvh_nodes.size(); ++i)
@@ -647,7 +689,7 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_bgroups, bgroups, &d.bgroups)) return rc;
     d.n_bgroups = (int)bgroups.size();
     d.bvh_has_bez = bvh_has_bez ? 1 : 0;
-    d.bvh_extent = bvh_extent;
+    d.bvh_pad = bvh_pad;
     if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
     d.n_bvh2 = (int)bvh2.size();

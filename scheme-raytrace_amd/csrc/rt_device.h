@@ -63,9 +63,10 @@ struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density,
 // parent so one visit tests two boxes.  Boxes are padded outward so culling is
 // conservative: the primitive tests are the exact f64 ones, the BVH only skips
 // primitives that cannot report a hit.  Child refs: >= 0 inner node, < 0 leaf
-// ~index into BvhLeaf.  Boxes are f32, rounded outward; the traversal's f32
-// slab test widens each axis interval by a per-ray bound on its rounding error
-// (box_ray), so culling stays conservative.
+// ~index into BvhLeaf.  Boxes are f32, rounded outward and widened by an
+// absolute margin that covers the f32 slab test's rounding for any ray whose
+// origin lies within the scene's radius (see commit_scene), so culling stays
+// conservative.
 struct alignas(64) BvhNode2 { float lbox[6]; float rbox[6]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
 constexpr int kLaneStack = 32;                 // per-lane traversal stack (LDS, stride = block size)
@@ -103,7 +104,7 @@ struct DevScene {
     const BvhNode2* bvh2;  int32_t n_bvh2;
     const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)
     int32_t bvh_has_bez;                           // curves in the BVH: widen the box t range (see bvh_closest)
-    float bvh_extent;                              // max |coordinate| of the BVH root box
+    float bvh_pad;                                 // the margin baked into the f32 boxes (diagnostic)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;

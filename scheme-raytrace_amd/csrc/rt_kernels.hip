@@ -434,49 +434,40 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
 // Per-lane BVH traversal: every lane walks its own path through the BVH2
 // (child boxes tested at the parent, nearer child first, LDS stack with a
 // block-size stride so a wave's pushes hit 64 consecutive banks).
-// f32 slab test.  With O = fl32(o), I = fl32(1/d) and f32 arithmetic, each
-// computed slab end is within 4 ulps * (|box| + |o|) * |I| of the exact one;
-// s = (extent + |O|) * |I| * 2^-19 per axis covers that, so the widened
-// interval contains the exact slab interval of the (outward-rounded) box.
-struct BoxRay { float ox, oy, oz, ix, iy, iz, sx, sy, sz; };
+// f32 slab test on t = fma(box, 1/d, -o/d).  Each computed slab end is
+// within 4 ulps * (|box| + |o|) * |1/d| of the exact one; the boxes carry an
+// absolute margin above that bound for any origin inside the scene radius
+// (commit_scene), so the test only culls boxes the ray misses.
+struct BoxRay { float ix, iy, iz, px, py, pz; };     // 1/d and o/d
 __device__ __forceinline__ float f32_up(const double x) {       // x >= 0 (a ray's t range)
     float f = (float)x;
     if ((double)f < x) f = __int_as_float(__float_as_int(f) + 1);
     return f;
 }
-__device__ __forceinline__ BoxRay box_ray(const v3 o, const v3 d, const float extent) {
-    BoxRay b;
+__device__ __forceinline__ BoxRay box_ray(const v3 o, const v3 d) {
     const double lim = 1e30;
-    b.ox = (float)o.x; b.oy = (float)o.y; b.oz = (float)o.z;
-    b.ix = (float)fmax(fmin(1.0 / d.x, lim), -lim);
-    b.iy = (float)fmax(fmin(1.0 / d.y, lim), -lim);
-    b.iz = (float)fmax(fmin(1.0 / d.z, lim), -lim);
-    const float k = 1.0f / 524288.0f;                      // 2^-19
-    b.sx = (extent + fabsf(b.ox)) * fabsf(b.ix) * k;
-    b.sy = (extent + fabsf(b.oy)) * fabsf(b.iy) * k;
-    b.sz = (extent + fabsf(b.oz)) * fabsf(b.iz) * k;
+    const double ix = fmax(fmin(1.0 / d.x, lim), -lim);
+    const double iy = fmax(fmin(1.0 / d.y, lim), -lim);
+    const double iz = fmax(fmin(1.0 / d.z, lim), -lim);
+    BoxRay b;
+    b.ix = (float)ix; b.iy = (float)iy; b.iz = (float)iz;
+    b.px = (float)(o.x * ix); b.py = (float)(o.y * iy); b.pz = (float)(o.z * iz);
     return b;
 }
 __device__ __forceinline__ bool box_hit_t(const float* bx, const BoxRay& r, const float tcap, float& tnear) {
-    const float tx0 = (bx[0] - r.ox) * r.ix, tx1 = (bx[3] - r.ox) * r.ix;
-    const float ty0 = (bx[1] - r.oy) * r.iy, ty1 = (bx[4] - r.oy) * r.iy;
-    const float tz0 = (bx[2] - r.oz) * r.iz, tz1 = (bx[5] - r.oz) * r.iz;
-    tnear = fmaxf(fmaxf(fminf(tx0, tx1) - r.sx, fminf(ty0, ty1) - r.sy), fmaxf(fminf(tz0, tz1) - r.sz, 0.0f));
-    const float tfar = fminf(fminf(fmaxf(tx0, tx1) + r.sx, fmaxf(ty0, ty1) + r.sy), fminf(fmaxf(tz0, tz1) + r.sz, tcap));
+    const float tx0 = fmaf(bx[0], r.ix, -r.px), tx1 = fmaf(bx[3], r.ix, -r.px);
+    const float ty0 = fmaf(bx[1], r.iy, -r.py), ty1 = fmaf(bx[4], r.iy, -r.py);
+    const float tz0 = fmaf(bx[2], r.iz, -r.pz), tz1 = fmaf(bx[5], r.iz, -r.pz);
+    tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
     return tnear <= tfar;
 }
 
-// Leaves are postponed (Aila & Laine's speculative while-while): a lane that
-// reaches a leaf parks it and keeps traversing until every active lane of
-// the wave has a leaf parked (or has finished), then the wave tests its
-// leaves together, so the f64 sphere code runs with most lanes active.
-// Deferring a leaf only delays the shrinking of `closest`, which culls less;
-// the closest hit is unchanged.
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d);
-    const BoxRay br = box_ray(o, d, sc.bvh_extent);
+    const BoxRay br = box_ray(o, d);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int sp = 0;
@@ -533,7 +524,7 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
                                                 BezWave& W) {
     const double a = dot(d, d);
-    const BoxRay br = box_ray(o, d, sc.bvh_extent);
+    const BoxRay br = box_ray(o, d);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     const double tscale = fmax(1.0, 1.0 / sqrt(a));
     const uint32_t lane = threadIdx.x & 63u;
