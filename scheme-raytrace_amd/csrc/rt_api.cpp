@@ -750,6 +750,11 @@ uint32_t tail_threshold() {
     const char* e = std::getenv("RTAMD_TAIL_PATHS");
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 32768u;
 }
+uint32_t tail_divisor() {
+    const char* e = std::getenv("RTAMD_TAIL_DIV");
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 128ul;
+    return v ? (uint32_t)v : 1u;
+}
 
 constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 5 * sizeof(uint32_t);
 
@@ -807,8 +812,8 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     constexpr int kIters = kMaxDepth + 4;
     HIPCHK(s->counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
     HIPCHK(s->queues.ensure(scap * 4 * sizeof(uint32_t)));
-    HIPCHK(s->seg_tail.ensure(sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(s->seg_tail.p, 0, sizeof(unsigned long long), stream));
+    HIPCHK(s->seg_tail.ensure(2 * sizeof(unsigned long long)));   // tail segments, next tail path
+    HIPCHK(hipMemsetAsync(s->seg_tail.p, 0, 2 * sizeof(unsigned long long), stream));
     if (!s->h_counts) HIPCHK(hipHostMalloc((void**)&s->h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
     if (s->profiling && !s->ev[0])
         for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
@@ -830,7 +835,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         rp.B = npix * S;
         // below the tail threshold one k_finish launch completes every
         // remaining path (extend + shade looped per thread)
-        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / 128u);
+        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / tail_divisor());
         HIPCHK(hipMemsetAsync(s->counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), stream));
         HIPCHK(launch_raygen(s->dev, rp, A, stream));
         PathState* cur = &A;
@@ -842,6 +847,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             if (depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
             if (n <= tail) {
                 if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
+                HIPCHK(hipMemsetAsync(s->seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), stream));
                 HIPCHK(launch_finish(s->dev, rp, *cur, view, n, s->seg_tail.as<unsigned long long>(), stream));
                 if (s->profiling) {
                     HIPCHK(hipEventRecord(s->ev[1], stream));

@@ -23,6 +23,7 @@
 // draw counter, consumed in the reference's order.
 #include <hip/hip_runtime.h>
 #include "rt_device.h"
+#include <cstdlib>
 
 namespace rtamd {
 
@@ -1176,20 +1177,39 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 template <int LS, int F>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
-                                                unsigned long long* __restrict__ seg_count) {
+                                                unsigned long long* __restrict__ tail_ctl) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_lstack[256 * LS];
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
     stage_perlin(sc, P);
-    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    // Persistent lanes: a lane whose path ended takes the next unstarted one
+    // (one atomic per wave per refill), so a wave is not held by its longest
+    // path while its other lanes idle.  tail_ctl[0] counts segments,
+    // tail_ctl[1] is the next path index.
+    unsigned int* next = reinterpret_cast<unsigned int*>(tail_ctl + 1);
+    const QMap qm = qmap(in);
+    const uint32_t lane = threadIdx.x & 63u;
     uint32_t segs = 0;
-    if (k < n) {
-        PathRegs p;
-        load_path(st, qphys(qmap(in), k), p);
-        v3 L;
-        for (;;) {
+    bool active = false, exhausted = false;
+    PathRegs p;
+    for (;;) {
+        const unsigned long long need = __ballot(!active);
+        if (need && !exhausted) {
+            uint32_t base = 0;
+            const uint32_t cnt = (uint32_t)__popcll(need);
+            const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;
+            if (lane == leader) base = atomicAdd(next, cnt);
+            base = __shfl(base, (int)leader, 64);
+            if (base + cnt >= n) exhausted = true;
+            if (!active) {
+                const uint32_t k = base + lanes_below(need);
+                if (k < n) { load_path(st, qphys(qm, k), p); active = true; }
+            }
+        }
+        if (__ballot(active) == 0ull) break;
+        if (active) {
             double t;
             ++segs;
             Rng g;
@@ -1197,14 +1217,16 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
             const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
                                                 &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g);
             if (MED) p.rng = g.ctr;
-            if (leaf < 0) { L = sky_radiance(sc, p.d); break; }
-            if (!shade_hit<-1>(sc, P, rp, p, t, leaf, L)) break;
+            v3 L;
+            bool cont = false;
+            if (leaf < 0) L = sky_radiance(sc, p.d);
+            else cont = shade_hit<-1>(sc, P, rp, p, t, leaf, L);
+            if (!cont) { write_sample(rp, p, L); active = false; }
         }
-        write_sample(rp, p, L);
     }
     // segment statistics: wave sum, one atomic per wave
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
-    if ((threadIdx.x & 63u) == 0u && segs) atomicAdd(seg_count, (unsigned long long)segs);
+    if (lane == 0u && segs) atomicAdd(tail_ctl, (unsigned long long)segs);
 }
 
 // =====================================================================
@@ -1240,6 +1262,14 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     const uint32_t blocks = (rp.B + 255u) / 256u;
     hipLaunchKernelGGL(k_raygen, dim3(blocks), dim3(256), 0, s, sc, rp, st);
     return hipGetLastError();
+}
+static uint32_t finish_blocks() {            // persistent tail grid (RTAMD_FINISH_BLOCKS)
+    static const uint32_t v = [] {
+        const char* e = std::getenv("RTAMD_FINISH_BLOCKS");
+        const long b = e ? std::atol(e) : 512;
+        return (uint32_t)(b > 0 ? b : 512);
+    }();
+    return v;
 }
 static int scene_features(const DevScene& sc) {
     return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
@@ -1287,7 +1317,8 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
 }
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, unsigned long long* seg_count, hipStream_t s) {
-    const uint32_t blocks = (n + 255u) / 256u;
+    uint32_t blocks = (n + 255u) / 256u;
+    if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
 #define RT_FINISH(LS, F) \
     hipLaunchKernelGGL((k_finish<LS, F>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count)
 #define RT_FINISH_F(F) do { if (sc.lane_stack <= kLaneStackSmall) RT_FINISH(kLaneStackSmall, F); else RT_FINISH(kLaneStack, F); } while (0)
