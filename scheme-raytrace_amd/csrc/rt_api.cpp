@@ -705,6 +705,8 @@ int commit_scene(Scene* s, int world) {
     d.n_mats = (int)s->mats.size(); d.n_texs = (int)s->texs.size();
     for (int k = 0; k < kLeafTypes; ++k) d.leaf_base[k] = base[k];
     d.has_perlin = s->have_perlin ? 1 : 0;
+    d.has_noise_tex = 0;
+    for (const auto& t : s->texs) if (t.type == TEX_NOISE || t.type == TEX_MARBLE) d.has_noise_tex = 1;
     if (s->have_perlin) {
         if (int rc = upload(s->d_ranvec, s->ranvec, &d.ranvec)) return rc;
         if (int rc = upload(s->d_perm, s->perm, &d.perm)) return rc;
@@ -752,7 +754,7 @@ uint32_t tail_threshold() {
 }
 uint32_t tail_divisor() {
     const char* e = std::getenv("RTAMD_TAIL_DIV");
-    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 128ul;
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 32ul;
     return v ? (uint32_t)v : 1u;
 }
 

@@ -114,6 +114,7 @@ struct DevScene {
     const double* ranvec;                      // 256*3 (Perlin)
     const int32_t* perm;                       // 3*256 (x, y, z)
     int32_t has_perlin;
+    int32_t has_noise_tex;                     // some texture is noise / marble
     int32_t sky;                               // 0 gradient, 1 black
     int32_t mat_mask;                          // bit t set <=> some material of type t exists
     DevCamera cam;

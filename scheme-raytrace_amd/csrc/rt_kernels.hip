@@ -992,6 +992,8 @@ __device__ __forceinline__ double perlin_turb(const PerlinLds& P, v3 p) {       
     }
     return fabs(acc);
 }
+// PN = false compiles the noise / marble cases out (scenes without them)
+template <bool PN>
 __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, int id, v3 p) {   // texture.scm
     for (int guard = 0; guard < 64; ++guard) {
         const DevTexture t = sc.texs[id];
@@ -1001,6 +1003,7 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
             id = (sines < 0.0) ? t.b : t.a;
             continue;
         }
+        if (!PN) return mk(0.0, 0.0, 0.0);
         if (t.type == TEX_NOISE) {                                   // :25-28
             const double nz = perlin_noise(P, p * t.scale);
             return mk(1.0, 1.0, 1.0) * nz;
@@ -1019,7 +1022,7 @@ __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - n * (2.0 * dot(v,
 // queue holds (compile-time; -1 = any, used by the tail kernel).  Returns true
 // if the path continues (p holds the scattered ray, new throughput, depth+1);
 // otherwise L is the terminal radiance (emission or 0).
-template <int MATF>
+template <int MATF, bool PN = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
                                           PathRegs& p, const double t, const int32_t leaf, v3& L) {
     L = mk(0.0, 0.0, 0.0);
@@ -1055,7 +1058,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     const v3 rdir = p.d;
     const bool can_continue = p.depth < (uint32_t)kMaxDepth;
     if (mt == MAT_DIFFUSE_LIGHT) {                           // material.scm:103-111
-        if (dot(nrm, rdir) < 0.0) L = tex_value(sc, P, m.tex, pt);
+        if (dot(nrm, rdir) < 0.0) L = tex_value<PN>(sc, P, m.tex, pt);
         return false;
     }
     if (!can_continue) return false;                         // depth cap (main.scm:112,119)
@@ -1085,7 +1088,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         if (cosine < 0.0) cosine = 0.0;
         const double spdf = cosine / kPi;                    // scattering-pdf
         const double ipdf = 1.0 / pdf;
-        const v3 att = tex_value(sc, P, m.tex, pt);
+        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
         // forward form of  e + ((att*spdf) (*) L_next) * (1/pdf)  (main.scm:113-118)
         p.T = mk((p.T.x * (att.x * spdf)) * ipdf, (p.T.y * (att.y * spdf)) * ipdf,
                  (p.T.z * (att.z * spdf)) * ipdf);
@@ -1100,7 +1103,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         }
         const v3 sd = reflected + s * m.fuzz;
         if (!(dot(sd, nrm) > 0.0)) return false;             // absorbed: emitted 0
-        const v3 att = tex_value(sc, P, m.tex, pt);
+        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
         p.T = p.T * att;
         p.d = sd;
     } else {                                                 // dielectric material.scm:76-101 (R2)
@@ -1131,8 +1134,9 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     return true;
 }
 
+template <bool PN = true>
 __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
-    if (sc.has_perlin) {   // the Perlin tables (perlin.scm:32-36 data) into LDS
+    if (PN && sc.has_perlin) {   // the Perlin tables (perlin.scm:32-36 data) into LDS
         for (int k = threadIdx.x; k < 768; k += blockDim.x) { P.ranvec[k] = sc.ranvec[k]; P.perm[k] = sc.perm[k]; }
         __syncthreads();
     }
@@ -1141,14 +1145,14 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 // =====================================================================
 // k_shade<MAT> — one material's queue; survivors compacted into `out`
 // =====================================================================
-template <int MAT>
+template <int MAT, bool PN>
 __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderParams rp, const PathState in,
                                                const HitBuf hit, const uint32_t* __restrict__ queue,
                                                const QView qv, PathState out, uint32_t* __restrict__ out_counts,
                                                uint32_t shard_cap) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
-    stage_perlin(sc, P);
+    stage_perlin<PN>(sc, P);
     const QMap qm = qmap(qv);
     uint32_t n = 0;
 #pragma unroll
@@ -1161,7 +1165,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
             const uint32_t i = queue[qphys(qm, k)];
             load_path(in, i, p);
             v3 L;
-            alive = shade_hit<MAT>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
+            alive = shade_hit<MAT, PN>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
@@ -1299,20 +1303,16 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > 4096u) blocks = 4096u;
     if (blocks == 0u) blocks = kShards;
+#define RT_SHADE(M, PN) \
+    hipLaunchKernelGGL((k_shade<M, PN>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap)
+    const bool pn = sc.has_noise_tex != 0;
     switch (mat) {
-    case MAT_LAMBERTIAN:
-        hipLaunchKernelGGL(k_shade<MAT_LAMBERTIAN>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
-        break;
-    case MAT_METAL:
-        hipLaunchKernelGGL(k_shade<MAT_METAL>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
-        break;
-    case MAT_DIELECTRIC:
-        hipLaunchKernelGGL(k_shade<MAT_DIELECTRIC>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
-        break;
-    default:
-        hipLaunchKernelGGL(k_shade<MAT_DIFFUSE_LIGHT>, dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap);
-        break;
+    case MAT_LAMBERTIAN: if (pn) RT_SHADE(MAT_LAMBERTIAN, true); else RT_SHADE(MAT_LAMBERTIAN, false); break;
+    case MAT_METAL: if (pn) RT_SHADE(MAT_METAL, true); else RT_SHADE(MAT_METAL, false); break;
+    case MAT_DIELECTRIC: RT_SHADE(MAT_DIELECTRIC, false); break;          // attenuation is constant 1
+    default: if (pn) RT_SHADE(MAT_DIFFUSE_LIGHT, true); else RT_SHADE(MAT_DIFFUSE_LIGHT, false); break;
     }
+#undef RT_SHADE
     return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
