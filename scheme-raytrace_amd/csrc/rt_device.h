@@ -69,8 +69,7 @@ struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density,
 // conservative.
 struct alignas(64) BvhNode2 { float lbox[6]; float rbox[6]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
-constexpr int kLaneStack = 32;                 // per-lane traversal stack (LDS, stride = block size)
-constexpr int kLaneStackSmall = 12;            // kernel variant for BVHs at most 12 levels deep
+constexpr int kLaneStack = 32;                 // max per-lane traversal stack (dynamic LDS, stride = block size)
 
 // Shade-side per-leaf record (indexed by leaf id).
 struct LeafInfo {

@@ -912,12 +912,13 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
 // the spot (sky); hits are appended to the queue of their material type so
 // each shade kernel runs one material's code (wavefront material queues).
 // =====================================================================
-template <int LS, int F>
+template <int F>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                 uint32_t* __restrict__ queues, uint32_t qstride,
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t s_lstack[256 * LS];
+    extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
+    const int LS = sc.lane_stack;
     __shared__ uint32_t s_cnt[4 * 16 + 4];
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
@@ -1178,12 +1179,13 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
-template <int LS, int F>
+template <int F>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl) {
     __shared__ PerlinLds P;
-    __shared__ uint32_t s_lstack[256 * LS];
+    extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
+    const int LS = sc.lane_stack;
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
@@ -1282,10 +1284,10 @@ hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathS
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
                          uint32_t* counts, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
-#define RT_EXTEND(LS, F)                                                                                     \
-    hipLaunchKernelGGL((k_extend<LS, F>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, hit, queues,     \
+    const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+#define RT_EXTEND_F(F)                                                                                      \
+    hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit, queues,     \
                        qstride, shard_cap, counts)
-#define RT_EXTEND_F(F) do { if (sc.lane_stack <= kLaneStackSmall) RT_EXTEND(kLaneStackSmall, F); else RT_EXTEND(kLaneStack, F); } while (0)
     switch (scene_features(sc)) {
     case 0: RT_EXTEND_F(0); break;
     case 1: RT_EXTEND_F(1); break;
@@ -1293,7 +1295,6 @@ hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathS
     default: RT_EXTEND_F(3); break;
     }
 #undef RT_EXTEND_F
-#undef RT_EXTEND
     return hipGetLastError();
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
@@ -1319,9 +1320,9 @@ hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathS
                          uint32_t n, unsigned long long* seg_count, hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
     if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
-#define RT_FINISH(LS, F) \
-    hipLaunchKernelGGL((k_finish<LS, F>), dim3(blocks), dim3(256), 0, s, sc, rp, st, in, n, seg_count)
-#define RT_FINISH_F(F) do { if (sc.lane_stack <= kLaneStackSmall) RT_FINISH(kLaneStackSmall, F); else RT_FINISH(kLaneStack, F); } while (0)
+    const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+#define RT_FINISH_F(F) \
+    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count)
     switch (scene_features(sc)) {
     case 0: RT_FINISH_F(0); break;
     case 1: RT_FINISH_F(1); break;
@@ -1329,7 +1330,6 @@ hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathS
     default: RT_FINISH_F(3); break;
     }
 #undef RT_FINISH_F
-#undef RT_FINISH
     return hipGetLastError();
 }
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {
