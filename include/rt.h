@@ -107,6 +107,12 @@ int rt_make_camera(const double lookfrom[3], const double lookat[3], const doubl
                    double vfov_deg, double aspect, double aperture, double focus_dist,
                    double time0, double time1, double out_cam[RT_CAMERA_DOUBLES]);
 int rt_set_camera(int scene, const double cam[RT_CAMERA_DOUBLES]);
+/* Extension (pdf.scm:18-41): lambertian bounces sample the mixture of
+ * (hitable-pdf light p) and (cosine-pdf normal), with g:pdf-value / g:random defined for an axis rect
+ * or a sphere as in "The Rest of Your Life".  light_obj = a rect or sphere object (flips allowed),
+ * -1 = off (the reference's own cosine sampling).  The reference never wires pdf.scm, so this path
+ * is checked against the oracle's restatement only. */
+int rt_set_light_sampling(int scene, int light_obj);
 int rt_set_sky(int scene, int sky);
 /* Perlin tables (perlin.scm:32-36): the reference draws them from the global
  * RNG at module load; here they are data.  ranvec: 256 unit vec3, perm: 256

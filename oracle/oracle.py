@@ -59,6 +59,8 @@ def lib():
                              ctypes.c_int], ctypes.c_int),
             "orc_set_camera": ([V, _dp], None),
             "orc_set_sky": ([V, ctypes.c_int], None),
+            "orc_set_light_sampling": ([V, ctypes.c_int], None),
+            "orc_light_pdf_value": ([V, _dp, _dp], ctypes.c_double),
             "orc_set_world": ([V, ctypes.c_int], None),
             "orc_set_perlin_tables": ([V, _dp, _ip, _ip, _ip], None),
             "orc_make_camera": ([_dp, _dp, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
@@ -179,6 +181,12 @@ class OracleScene:
 
     def set_camera(self, slots):
         self.L.orc_set_camera(self.s, _dv(slots))
+
+    def set_light(self, obj):
+        self.L.orc_set_light_sampling(self.s, obj)
+
+    def light_pdf_value(self, o, v):
+        return self.L.orc_light_pdf_value(self.s, _dv(o), _dv(v))
 
     def set_sky(self, code):
         self.L.orc_set_sky(self.s, code)

@@ -136,6 +136,7 @@ typedef struct {
     int* kids; int nkids, ckids;
     double cam[24];
     int sky, world;
+    int light;                          /* light-sampling target object (-1: off), pdf.scm extension */
     v3 ranvec[256];
     int perm_x[256], perm_y[256], perm_z[256];
     int have_perlin;
@@ -152,6 +153,7 @@ typedef struct {
 orc_scene* orc_scene_new(void) {
     orc_scene* s = calloc(1, sizeof *s);
     s->world = -1;
+    s->light = -1;
     return s;
 }
 void orc_scene_free(orc_scene* s) {
@@ -293,6 +295,7 @@ int orc_add_bezier_array(orc_scene* s, const double* cps, int n, double width, i
 
 void orc_set_camera(orc_scene* s, const double cam[24]) { memcpy(s->cam, cam, sizeof s->cam); }
 void orc_set_sky(orc_scene* s, int sky) { s->sky = sky; }
+void orc_set_light_sampling(orc_scene* s, int obj) { s->light = obj; }
 void orc_set_world(orc_scene* s, int world) { s->world = world; }
 void orc_set_perlin_tables(orc_scene* s, const double* ranvec, const int32_t* px, const int32_t* py,
                            const int32_t* pz) {
@@ -803,6 +806,72 @@ static v3 sky(const orc_scene* s, ray_t r) {
     return vadd(vscale(V(1, 1, 1), 1 - t), vscale(V(0.5, 0.7, 1.0), t));
 }
 
+/* ------------------------------------------- pdf.scm light sampling (f2)
+ * pdf.scm (make-cosine-pdf :18-26, make-hitable-pdf :28-32, make-mixture-pdf
+ * :34-41) calls g:pdf-value / g:random, which geometry.scm never defines, and
+ * main.scm never wires the pdfs into `color`.  This extension defines them as
+ * "The Rest of Your Life" does, for an axis rect or a sphere, and uses the
+ * mixture (light, cosine) for lambertian bounces.  Scheme semantics are kept:
+ * onb `local` is the syntax-rules macro, so a sampler passed to it runs three
+ * times (Q29).  Not pinned against the reference (it has no such path). */
+static const orc_obj* light_obj(const orc_scene* s) {
+    const orc_obj* o = &s->obj[s->light];
+    while (o->type == OBJ_FLIP) o = &s->obj[o->child];
+    return o;
+}
+/* g:pdf-value: density of direction v from origin o */
+static double light_pdf_value(const orc_scene* s, v3 o, v3 v) {
+    const orc_obj* L = light_obj(s);
+    hitrec rec;
+    ray_t r = {o, v, 0.0};
+    if (L->type == OBJ_RECT) {
+        if (!rect_hit(L, r, ORC_TMIN, ORC_TMAX, &rec)) return 0;
+        double area = (L->a1 - L->a0) * (L->b1 - L->b0);
+        double distance_squared = rec.t * rec.t * vdot(v, v);
+        double cosine = fabs(vdot(v, rec.n) / vlength(v));
+        return distance_squared / (cosine * area);
+    }
+    if (!sphere_hit(L->c0, L->r, L->mat, r, ORC_TMIN, ORC_TMAX, &rec)) return 0;
+    v3 oc = vsub(L->c0, o);
+    double cos_theta_max = sqrt(1 - L->r * L->r / vdot(oc, oc));
+    double solid_angle = 2 * ORC_PI * (1 - cos_theta_max);
+    return 1 / solid_angle;
+}
+static v3 random_to_sphere(double radius, double distance_squared, orc_rng* g) {
+    double r1 = orc_random_real(g);
+    double r2 = orc_random_real(g);
+    double z = 1 + r2 * (sqrt(1 - radius * radius / distance_squared) - 1);
+    double phi = 2 * ORC_PI * r1;
+    double x = cos(phi) * sqrt(1 - z * z);
+    double y = sin(phi) * sqrt(1 - z * z);
+    return V(x, y, z);
+}
+/* g:random: a direction from o toward the light */
+static v3 light_random(const orc_scene* s, v3 o, orc_rng* g) {
+    const orc_obj* L = light_obj(s);
+    if (L->type == OBJ_RECT) {
+        double a = L->a0 + orc_random_real(g) * (L->a1 - L->a0);
+        double b = L->b0 + orc_random_real(g) * (L->b1 - L->b0);
+        v3 pnt = (L->axis == 0) ? V(a, b, L->k) : (L->axis == 1) ? V(a, L->k, b) : V(L->k, a, b);
+        return vsub(pnt, o);
+    }
+    v3 direction = vsub(L->c0, o);
+    double distance_squared = vdot(direction, direction);
+    onb_t uvw = make_onb_from_w(direction);
+    double x = random_to_sphere(L->r, distance_squared, g).x;       /* local: three evaluations (Q29) */
+    double y = random_to_sphere(L->r, distance_squared, g).y;
+    double z = random_to_sphere(L->r, distance_squared, g).z;
+    return onb_local(uvw, V(x, y, z));
+}
+/* make-cosine-pdf's value (pdf.scm:19-23) */
+static double cosine_pdf_value(onb_t uvw, v3 dir) {
+    double cosine = vdot(vunit(dir), uvw.w);
+    return (cosine > 0) ? cosine / ORC_PI : 0;
+}
+double orc_light_pdf_value(const orc_scene* s, const double o[3], const double v[3]) {
+    return light_pdf_value(s, V(o[0], o[1], o[2]), V(v[0], v[1], v[2]));
+}
+
 typedef struct { uint64_t segments; int max_depth; } orc_counters;
 
 /* main.scm:100-121 — recursive colour */
@@ -818,6 +887,30 @@ static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters
     const orc_mat* m = &s->mat[rec.mat];
     switch (m->type) {
     case MAT_LAMBERTIAN: {                                              /* material.scm:24-39 */
+        if (s->light >= 0) {
+            /* mixture of (hitable-pdf light p) and (cosine-pdf normal), pdf.scm:34-41 */
+            onb_t uvw = make_onb_from_w(rec.n);
+            v3 dir;
+            if (orc_random_real(g) < 0.5) {
+                dir = light_random(s, rec.p, g);
+            } else {
+                double cx = random_cosine_direction(g).x;
+                double cy = random_cosine_direction(g).y;
+                double cz = random_cosine_direction(g).z;
+                dir = onb_local(uvw, V(cx, cy, cz));
+            }
+            ray_t scattered = {rec.p, dir, 0.0};
+            double pdf_val = 0.5 * light_pdf_value(s, rec.p, dir) + 0.5 * cosine_pdf_value(uvw, dir);
+            v3 att = tex_value(s, m->tex, 0, 0, rec.p);
+            if (depth < ORC_MAX_DEPTH) {
+                double cosine = vdot(rec.n, vunit(scattered.d));
+                if (cosine < 0) cosine = 0;
+                double spdf = cosine / ORC_PI;
+                v3 L = color(s, scattered, depth + 1, g, cnt);
+                return vadd(V(0, 0, 0), vscale(vmul(vscale(att, spdf), L), 1 / pdf_val));
+            }
+            return V(0, 0, 0);
+        }
         onb_t uvw = make_onb_from_w(rec.n);
         /* (local uvw (random-cosine-direction)) — `local` is a syntax-rules
          * macro (onb.scm:27-36) that substitutes its argument EXPRESSION into

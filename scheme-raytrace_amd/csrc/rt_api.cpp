@@ -88,6 +88,7 @@ struct Scene {
     double cam[RT_CAMERA_DOUBLES] = {0};
     bool have_cam = false;
     int sky = RT_SKY_GRADIENT;
+    int light = -1;                   // rt_set_light_sampling target (-1: off)
     std::vector<double> ranvec;
     std::vector<int32_t> perm;
     bool have_perlin = false;
@@ -712,6 +713,18 @@ int commit_scene(Scene* s, int world) {
         if (int rc = upload(s->d_perm, s->perm, &d.perm)) return rc;
     }
     d.sky = s->sky;
+    std::memset(&d.light, 0, sizeof d.light);
+    if (s->light >= 0) {
+        const Obj* L = &s->objs[s->light];
+        while (L->type == O_FLIP) L = &s->objs[L->child];
+        if (L->type == O_RECT) {
+            d.light.type = LIGHT_RECT; d.light.axis = L->axis;
+            d.light.a0 = L->a0; d.light.a1 = L->a1; d.light.b0 = L->b0; d.light.b1 = L->b1; d.light.k = L->k;
+        } else {
+            d.light.type = LIGHT_SPHERE;
+            d.light.cx = L->c0[0]; d.light.cy = L->c0[1]; d.light.cz = L->c0[2]; d.light.r = L->r;
+        }
+    }
     d.mat_mask = 0;
     for (const auto& m : s->mats) d.mat_mask |= 1 << m.type;
     const double* cm = s->cam;
@@ -1096,6 +1109,17 @@ int rt_add_constant_medium(int scene, int boundary, double density, int albedo_t
     s->mats.push_back(m);
     Obj o; o.type = O_MEDIUM; o.child = boundary; o.r = density; o.mat = (int)s->mats.size() - 1;
     return push_obj(s, std::move(o), out);
+}
+int rt_set_light_sampling(int scene, int light_obj) {
+    SCENE_OR_FAIL(s, scene);
+    if (light_obj < 0) { s->light = -1; return 0; }
+    if (check_obj(s, light_obj)) return 1;
+    const Obj* L = &s->objs[light_obj];
+    while (L->type == O_FLIP) L = &s->objs[L->child];
+    if (L->type != O_RECT && L->type != O_SPHERE)
+        return fail("rt_set_light_sampling: the light must be a rect or a sphere (optionally flipped)");
+    s->light = light_obj;
+    return 0;
 }
 int rt_add_flip_normals(int scene, int child, int* out) {
     SCENE_OR_FAIL(s, scene);

@@ -86,6 +86,15 @@ struct Chain { int32_t n, pad; ChainOpRec ops[kMaxChain]; };
 struct Group { int32_t type, chain, begin, end; };   // begin/end index the type array
                                                       // leaf id = leaf_base[type] + local
 
+// Light sampling target for the pdf.scm mixture (extension f2): an axis rect
+// (axis as LeafType rect order) or a sphere.  type 0 = off.
+struct DevLight {
+    int32_t type, axis, pad0, pad1;          // type: 0 off, 1 rect, 2 sphere
+    double a0, a1, b0, b1, k;                // rect
+    double cx, cy, cz, r;                    // sphere
+};
+enum { LIGHT_OFF = 0, LIGHT_RECT = 1, LIGHT_SPHERE = 2 };
+
 struct DevCamera {            // camera.scm:33-78 (the 10 slots)
     double llc[3], hor[3], ver[3], origin[3], w[3], u[3], v[3];
     double lens, t0, t1;
@@ -117,6 +126,7 @@ struct DevScene {
     int32_t sky;                               // 0 gradient, 1 black
     int32_t mat_mask;                          // bit t set <=> some material of type t exists
     DevCamera cam;
+    DevLight light;
 };
 
 // Wavefront path state, SoA, one slot per live path (ping-pong buffers).

@@ -1018,6 +1018,67 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
 
 __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - n * (2.0 * dot(v, n)); }  // material.scm:41-43
 
+// --------------------------------------------- light sampling (f2 extension)
+// g:pdf-value / g:random for the light, "Rest of Your Life" style (see
+// rt_oracle.c light_pdf_value / light_random for the restatement they match).
+__device__ __forceinline__ double light_pdf_value(const DevLight& L, const v3 o, const v3 v) {
+    if (L.type == LIGHT_RECT) {
+        double ok, dk, oa, da, ob, db;
+        v3 n;
+        if (L.axis == 0) { ok = o.z; dk = v.z; oa = o.x; da = v.x; ob = o.y; db = v.y; n = mk(0.0, 0.0, 1.0); }
+        else if (L.axis == 1) { ok = o.y; dk = v.y; oa = o.x; da = v.x; ob = o.z; db = v.z; n = mk(0.0, 1.0, 0.0); }
+        else { ok = o.x; dk = v.x; oa = o.y; da = v.y; ob = o.z; db = v.z; n = mk(1.0, 0.0, 0.0); }
+        const double t = (L.k - ok) / dk;
+        if (t < kTmin || t > kTmax) return 0.0;
+        const double A = oa + t * da, Bv = ob + t * db;
+        if (A < L.a0 || A > L.a1 || Bv < L.b0 || Bv > L.b1) return 0.0;
+        const double area = (L.a1 - L.a0) * (L.b1 - L.b0);
+        const double distance_squared = t * t * dot(v, v);
+        const double cosine = fabs(dot(v, n) / length(v));
+        return distance_squared / (cosine * area);
+    }
+    // sphere: hit test as geometry.scm:146-171, then 1 / solid angle of the cone
+    const v3 c = mk(L.cx, L.cy, L.cz);
+    const v3 oc = o - c;
+    const double a = dot(v, v), b = dot(oc, v), cc = dot(oc, oc) - L.r * L.r;
+    const double disc = b * b - a * cc;
+    if (disc <= 0.0) return 0.0;
+    double t = (-b - sqrt(disc)) / a;
+    if (!(kTmin < t && t < kTmax)) {
+        t = (-b + sqrt(disc)) / a;
+        if (!(kTmin < t && t < kTmax)) return 0.0;
+    }
+    const v3 co = c - o;
+    const double cos_theta_max = sqrt(1.0 - L.r * L.r / dot(co, co));
+    const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
+    return 1.0 / solid_angle;
+}
+__device__ __forceinline__ v3 random_to_sphere(const double radius, const double distance_squared, Rng& g) {
+    const double r1 = g.next();
+    const double r2 = g.next();
+    const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / distance_squared) - 1.0);
+    const double phi = 2.0 * kPi * r1;
+    return mk(cos(phi) * sqrt(1.0 - z * z), sin(phi) * sqrt(1.0 - z * z), z);
+}
+__device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g) {
+    if (L.type == LIGHT_RECT) {
+        const double a = L.a0 + g.next() * (L.a1 - L.a0);
+        const double b = L.b0 + g.next() * (L.b1 - L.b0);
+        const v3 pnt = (L.axis == 0) ? mk(a, b, L.k) : (L.axis == 1) ? mk(a, L.k, b) : mk(L.k, a, b);
+        return pnt - o;
+    }
+    const v3 direction = mk(L.cx, L.cy, L.cz) - o;
+    const double distance_squared = dot(direction, direction);
+    const v3 w = unit(direction);
+    const v3 aa = (fabs(w.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+    const v3 vv = unit(cross(w, aa));
+    const v3 uu = cross(w, vv);
+    const double x = random_to_sphere(L.r, distance_squared, g).x;      // local: three evaluations (Q29)
+    const double y = random_to_sphere(L.r, distance_squared, g).y;
+    const double z = random_to_sphere(L.r, distance_squared, g).z;
+    return (uu * x + vv * y) + w * z;
+}
+
 // ------------------------------------------------------------- shading
 // Hit record + material (material.scm:15-111).  MATF = the material type a
 // queue holds (compile-time; -1 = any, used by the tail kernel).  Returns true
@@ -1065,7 +1126,39 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     if (!can_continue) return false;                         // depth cap (main.scm:112,119)
     Rng g;
     g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
-    if (mt == MAT_LAMBERTIAN) {                              // material.scm:24-39
+    if (mt == MAT_LAMBERTIAN && sc.light.type != LIGHT_OFF) {
+        // pdf.scm mixture of (hitable-pdf light p) and (cosine-pdf normal)
+        // (extension f2; oracle: rt_oracle.c light_pdf_value / light_random)
+        const v3 axis2 = unit(nrm);
+        const v3 a = (fabs(axis2.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+        const v3 axis1 = unit(cross(axis2, a));
+        const v3 axis0 = cross(axis2, axis1);
+        const DevLight& Lt = sc.light;
+        v3 dir;
+        if (g.next() < 0.5) {
+            dir = light_random(Lt, pt, g);
+        } else {
+            const double r1 = g.next(), r2 = g.next();
+            const double r3 = g.next(), r4 = g.next();
+            (void)g.next();
+            const double r6 = g.next();
+            const double x = cos(2.0 * kPi * r1) * 2.0 * sqrt(r2);
+            const double y = sin(2.0 * kPi * r3) * 2.0 * sqrt(r4);
+            const double z = sqrt(1.0 - r6);
+            dir = (axis0 * x + axis1 * y) + axis2 * z;
+        }
+        double cz = dot(unit(dir), axis2);
+        const double cos_val = (cz > 0.0) ? cz / kPi : 0.0;
+        const double pdf_val = 0.5 * light_pdf_value(Lt, pt, dir) + 0.5 * cos_val;
+        double cosine = dot(nrm, unit(dir));
+        if (cosine < 0.0) cosine = 0.0;
+        const double spdf = cosine / kPi;
+        const double ipdf = 1.0 / pdf_val;
+        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
+        p.T = mk((p.T.x * (att.x * spdf)) * ipdf, (p.T.y * (att.y * spdf)) * ipdf,
+                 (p.T.z * (att.z * spdf)) * ipdf);
+        p.d = dir;
+    } else if (mt == MAT_LAMBERTIAN) {                       // material.scm:24-39
         // onb.scm:8-16
         const v3 axis2 = unit(nrm);
         const v3 a = (fabs(axis2.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);

@@ -75,6 +75,7 @@ _SIGNATURES = {
                        ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _c_double_p],
     "rt_set_camera": [ctypes.c_int, _c_double_p],
     "rt_set_sky": [ctypes.c_int, ctypes.c_int],
+    "rt_set_light_sampling": [ctypes.c_int, ctypes.c_int],
     "rt_set_perlin_tables": [ctypes.c_int, _c_double_p, _c_i32_p, _c_i32_p, _c_i32_p],
     "rt_scene_commit": [ctypes.c_int, ctypes.c_int],
     "rt_render": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,

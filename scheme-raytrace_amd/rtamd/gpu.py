@@ -128,6 +128,9 @@ class GpuBuilder:
     def set_camera(self, slots):
         call("rt_set_camera", self.scene, dvec(slots))
 
+    def set_light(self, obj):
+        call("rt_set_light_sampling", self.scene, obj)
+
     def set_sky(self, code):
         call("rt_set_sky", self.scene, code)
 

@@ -238,13 +238,24 @@ class Scene:
     (the reference's module-level +ranvec+/+perm-*+, perlin.scm:32-36).
     """
 
-    def __init__(self, obj_list, camera, sky_function, perlin=None):
+    def __init__(self, obj_list, camera, sky_function, perlin=None, light=None):
         self.obj_list = tuple(obj_list)
         for o in self.obj_list:
             _need(o, Hitable, "make-scene obj-list element")
         self.camera = camera
         self.sky_function = sky_function
         self.perlin = perlin
+        # extension (pdf.scm, SURVEY §8 f2): lambertian bounces sample the
+        # mixture of (hitable-pdf light p) and (cosine-pdf normal)
+        if light is not None:
+            _need(light, Hitable, "light-sampling target")
+            if light.kind == "flip":
+                inner = light.args[0]
+            else:
+                inner = light
+            if inner.kind not in ("rect", "sphere"):
+                raise ValueError("light sampling needs a rect or a sphere (optionally flipped)")
+        self.light = light
         self._handles = {}
 
     def uses_perlin(self):
@@ -265,11 +276,13 @@ class Scene:
         return False
 
 
-def make_scene(obj_list, camera, sky_function, perlin=None):
-    """g:make-scene (geometry.scm:52)."""
+def make_scene(obj_list, camera, sky_function, perlin=None, light=None):
+    """g:make-scene (geometry.scm:52).  ``light`` (extension, pdf.scm): an
+    object of obj_list (a rect or sphere, possibly flipped) that lambertian
+    bounces sample through the light/cosine mixture pdf."""
     if not isinstance(sky_function, SkyFunction):
         raise TypeError("make-scene: sky function must be sky_color or black (got %r)" % (sky_function,))
-    return Scene(obj_list, camera, sky_function, perlin)
+    return Scene(obj_list, camera, sky_function, perlin, light)
 
 
 def _need(x, cls, what):
@@ -355,6 +368,8 @@ def emit(scene, b):
 
     ids = [obj(o) for o in scene.obj_list]
     world = b.list(ids)
+    if getattr(scene, "light", None) is not None:
+        b.set_light(obj(scene.light))
     b.set_camera(scene.camera.slots())
     b.set_sky(scene.sky_function.code)
     if scene.uses_perlin():

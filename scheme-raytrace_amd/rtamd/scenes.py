@@ -132,6 +132,15 @@ def cornell_box(nx, ny):
     return g.make_scene(objs, cornell_camera_for(nx, ny), g.sky_color)
 
 
+def cornell_mixture(nx, ny):
+    """cornell-box with the pdf.scm mixture (extension f2, config C4's
+    "mixture/cosine importance sampling"): lambertian bounces sample the
+    ceiling light and the cosine lobe half and half."""
+    sc = cornell_box(nx, ny)
+    light = sc.obj_list[2]                      # (g:flip-normals (g:make-xz-rect 213 343 227 332 554 light))
+    return g.make_scene(sc.obj_list, sc.camera, sc.sky_function, light=light)
+
+
 def line_upped_spheres(nx, ny, rr):
     """line-upped-spheres (main.scm:177-191)."""
     out = []
@@ -301,6 +310,7 @@ SCENES = {
     "test_bezier": test_bezier,
     "cornell_bezier": cornell_bezier,
     "cornell_smoke": cornell_smoke,
+    "cornell_mixture": cornell_mixture,
     "klein": klein_scene,
     "cornell_klein": cornell_klein,
     "curves": cornell_curves,

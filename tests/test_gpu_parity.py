@@ -49,6 +49,7 @@ def _both(scene, nx, ny, spp, oracle_mod, spp_begin=0, seed=SEED):
     ("curves_small", 64, 36, 2),
     ("cornell_smoke", 48, 48, 8),
     ("cornell_klein", 32, 32, 2),
+    ("cornell_mixture", 48, 48, 8),
 ])
 def test_scene_parity(name, nx, ny, spp, gpu_ctx, oracle_mod):
     scene = scenes.SCENES[name](nx, ny)
@@ -268,5 +269,22 @@ def test_media_in_list_order(gpu_ctx, oracle_mod):
     acc, ref = _both(sc, nx, ny, spp, oracle_mod)
     rms, dmax, nbad, npx = _compare(acc, ref, spp)
     print("media order: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)
+
+
+def test_sphere_light_mixture(gpu_ctx, oracle_mod):
+    """pdf.scm mixture toward a sphere light (extension f2): GPU vs oracle."""
+    from rtamd import scene as g
+    from rtamd.camera import make_camera
+    lam = g.make_lambertian(g.constant_texture((0.6, 0.5, 0.4)))
+    light = g.make_sphere((0, 3, 0), 0.7, g.make_diffuse_light(g.constant_texture((4, 4, 4))))
+    sc = g.make_scene([g.make_sphere((0, -1000, 0), 1000, lam), g.make_sphere((0, 1, 0), 1, lam), light],
+                      make_camera((0, 1.5, 6), (0, 1, 0), (0, 1, 0), 40, 1.5, 0, 1, 0, 1), g.black, light=light)
+    nx, ny, spp = 60, 40, 8
+    acc, ref = _both(sc, nx, ny, spp, oracle_mod)
+    rms, dmax, nbad, npx = _compare(acc, ref, spp)
+    print("sphere-light mixture: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    assert np.isfinite(acc).all()
     assert rms <= RMS_TOL
     assert nbad <= max(2, npx // 200)
