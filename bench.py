@@ -86,11 +86,12 @@ def cpu_baseline(scene, nx, ny, seed, budget_s):
                                                                  t_used)}
 
 
-SCENE_CONFIG = {"cover": "C2", "cover_marble": "C3", "cornell": "C4", "curves": "C5"}
+SCENE_CONFIG = {"cover": "C2", "cover_marble": "C3", "cornell": "C4", "cornell_mixture": "C4-mixture", "curves": "C5"}
 SCENE_DATA = {
     "cover": "RTIOW cover scene (random-scene, main.scm:31-89 + repairs R1/R3) generated from host seed 0x5EED0001",
     "cover_marble": "cover scene with a marble ground (C3), host seed 0x5EED0001, Perlin seed 0x5EED0003",
     "cornell": "cornell-box (main.scm:330-351)",
+    "cornell_mixture": "cornell-box with pdf.scm light/cosine mixture sampling toward the ceiling light (extension f2)",
     "curves": "2^20 curves from seeded random polylines via points->bezier (numpy seed 0x5EED0005) in a BVH "
               "inside the cornell-bezier frame (main.scm:353-373)",
 }

@@ -901,6 +901,9 @@ static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters
             }
             ray_t scattered = {rec.p, dir, 0.0};
             double pdf_val = 0.5 * light_pdf_value(s, rec.p, dir) + 0.5 * cosine_pdf_value(uvw, dir);
+            /* a direction neither pdf can produce (a light sample that grazes
+             * past the light, below the surface) ends the path: no 0 * inf */
+            if (!(pdf_val > 0)) return V(0, 0, 0);
             v3 att = tex_value(s, m->tex, 0, 0, rec.p);
             if (depth < ORC_MAX_DEPTH) {
                 double cosine = vdot(rec.n, vunit(scattered.d));

@@ -1150,6 +1150,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         double cz = dot(unit(dir), axis2);
         const double cos_val = (cz > 0.0) ? cz / kPi : 0.0;
         const double pdf_val = 0.5 * light_pdf_value(Lt, pt, dir) + 0.5 * cos_val;
+        if (!(pdf_val > 0.0)) return false;                 // no 0 * inf: the path ends (L = 0)
         double cosine = dot(nrm, unit(dir));
         if (cosine < 0.0) cosine = 0.0;
         const double spdf = cosine / kPi;
