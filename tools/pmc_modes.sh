@@ -16,7 +16,7 @@ if [ "$MODE" = flat ]; then export RTAMD_BVH_MIN=1000000000; else export RTAMD_B
 i=0
 for P in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex k_extend -f csv -d $R/gpurun_out/pmc_${SCENE}_$MODE$i -o p -- \
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex ${KREGEX:-k_extend} -f csv -d $R/gpurun_out/pmc_${SCENE}_$MODE$i -o p -- \
     python3 bench.py --scene $SCENE --spp $SPP --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events \
     > gpurun_out/pmc_${SCENE}_$MODE$i.log 2>&1 || exit $?
 done
