@@ -4,19 +4,25 @@
 // wavefront over a pool of paths kept SoA in HBM:
 //
 //   k_raygen    trace-all jitter + cam:get-ray      main.scm:476-478, camera.scm:80-92
-//   k_extend    closest hit over the flattened       geometry.scm:14-56,146-215,376-543
-//               object tree (one segment per path);  main.scm:91-95,120
+//   k_extend<F> closest hit over the flattened       geometry.scm:14-56,146-215,376-673,
+//               object tree (one segment per path):  bezier.scm:13-223; main.scm:91-95,120
+//               per-lane BVH traversal, brute-force
+//               groups, wave-batched curve tests;
 //               misses finish with the sky, hits are
 //               appended to per-material queues
 //   k_shade<M>  hit record + material M's scatter /  material.scm:15-111, texture.scm,
-//               emission; survivors compacted with   perlin.scm, main.scm:100-121
-//               a wave64 ballot + mbcnt prefix and
-//               one atomic per wave
-//   k_finish    the depth tail: extend+shade looped  (same code, one thread per path)
-//               per thread for the last few paths
+//               emission; survivors compacted with   perlin.scm, pdf.scm (f2), main.scm:100-121
+//               a wave64 ballot + mbcnt prefix, an
+//               LDS scan and one atomic per block
+//   k_finish<F> the depth tail: extend+shade looped  (same code; persistent lanes refill
+//               per lane for the last paths           from the remaining path list)
 //   k_accumulate per-pixel running sum in sample     main.scm:480,488
 //               order (deterministic, no atomics)
 //   k_resolve_u8 correct-gamma + quantise            main.scm:481-491
+//
+// F selects the closest-hit features compiled in (kFeatCurves: curve batching
+// state; kFeatExtra: constant media and Klein limit sets, which draw random
+// numbers / march inside the hit test), so sphere scenes run lean kernels.
 //
 // All arithmetic is f64 like the reference's flonums.  Random numbers come
 // from a Philox4x32-10 stream keyed by (seed, pixel, sample) with a per-path
