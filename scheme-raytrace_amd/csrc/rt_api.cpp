@@ -823,7 +823,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     HIPCHK(s->hit_t.ensure(scap * sizeof(double)));
     HIPCHK(s->hit_leaf.ensure(scap * sizeof(int32_t)));
     HIPCHK(s->sb.ensure(cap * 3 * sizeof(double)));
-    constexpr int kCountsPerIter = 5 * kShards;   // 4 material queues + survivors, 8 shards each
+    constexpr int kCountsPerIter = 5 * kShards * kCntStride;   // 4 material queues + survivors, 8 shards each
     constexpr int kIters = kMaxDepth + 4;
     HIPCHK(s->counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
     HIPCHK(s->queues.ensure(scap * 4 * sizeof(uint32_t)));
@@ -878,15 +878,15 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
             HIPCHK(launch_extend(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt, stream));
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[1], stream));
-            uint32_t* surv = cnt + 4 * kShards;
+            uint32_t* surv = cnt + 4 * kShards * kCntStride;
             for (int mt = 0; mt < 4; ++mt) {
                 if (!(mat_mask & (1 << mt))) continue;
-                const QView qv{cnt + mt * kShards, (uint32_t)shard_cap};
+                const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
                 HIPCHK(launch_shade(mt, s->dev, rp, *cur, hit, queues + (size_t)mt * qstride, qv, n, *nxt, surv,
                                     (uint32_t)shard_cap, stream));
             }
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[2], stream));
-            HIPCHK(hipMemcpyAsync(s->h_counts + depth * kCountsPerIter, surv, kShards * sizeof(uint32_t),
+            HIPCHK(hipMemcpyAsync(s->h_counts + depth * kCountsPerIter, surv, kShards * kCntStride * sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             if (s->profiling) {
@@ -901,7 +901,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             if ((uint32_t)depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)depth;
             n = 0;
             for (int x = 0; x < kShards; ++x) {
-                const uint32_t c_x = s->h_counts[depth * kCountsPerIter + x];
+                const uint32_t c_x = s->h_counts[depth * kCountsPerIter + x * kCntStride];
                 if (c_x > shard_cap) return fail("internal: shard overflow");
                 n += c_x;
             }

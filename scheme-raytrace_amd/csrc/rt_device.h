@@ -143,6 +143,13 @@ struct HitBuf { double* t; int32_t* leaf; };
 // at [x*cap, x*cap + counts[x]).  Consumers see a virtual index space
 // 0..sum(counts)-1 (QView; counts == nullptr means "contiguous").
 constexpr int kShards = 8;
+// Counter k of a counter array lives at [k * kCntStride] (uint32 units): each
+// shard counter gets its own 128-B line, so the shards' atomics do not meet
+// in one L2 line.
+#ifndef RT_CNT_STRIDE
+#define RT_CNT_STRIDE 32
+#endif
+constexpr int kCntStride = RT_CNT_STRIDE;
 struct QView { const uint32_t* counts; uint32_t cap; };
 
 // Per-render-chunk parameters shared by the kernels.

@@ -868,7 +868,7 @@ __device__ __forceinline__ QMap qmap(const QView v) {
     m.contiguous = v.counts == nullptr;
     uint32_t acc = 0;
 #pragma unroll
-    for (int x = 0; x < kShards; ++x) { m.off[x] = acc; if (!m.contiguous) acc += v.counts[x]; }
+    for (int x = 0; x < kShards; ++x) { m.off[x] = acc; if (!m.contiguous) acc += v.counts[x * kCntStride]; }
     return m;
 }
 __device__ __forceinline__ uint32_t qphys(const QMap& m, uint32_t k) {
@@ -904,7 +904,7 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
         const int c = threadIdx.x;
         uint32_t tot = 0;
         for (uint32_t w = 0; w < nw; ++w) { const uint32_t v = s_cnt[c * 16 + w]; s_cnt[c * 16 + w] = tot; tot += v; }
-        s_cnt[NC * 16 + c] = tot ? atomicAdd(counts + c * kShards + shard, tot) : 0u;
+        s_cnt[NC * 16 + c] = tot ? atomicAdd(counts + (c * kShards + shard) * kCntStride, tot) : 0u;
     }
     __syncthreads();
     uint32_t slot = 0;
@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
     const QMap qm = qmap(qv);
     uint32_t n = 0;
 #pragma unroll
-    for (int x = 0; x < kShards; ++x) n += qv.counts[x];
+    for (int x = 0; x < kShards; ++x) n += qv.counts[x * kCntStride];
     for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
         const uint32_t k = base + threadIdx.x;
         bool alive = false;
