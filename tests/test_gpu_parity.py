@@ -288,3 +288,22 @@ def test_sphere_light_mixture(gpu_ctx, oracle_mod):
     assert np.isfinite(acc).all()
     assert rms <= RMS_TOL
     assert nbad <= max(2, npx // 200)
+
+
+def test_c_example_matches_python_host(gpu_ctx, tmp_path):
+    """The C-ABI example (examples/cornell.c) and the Python host render the
+    same cornell-box to the same PPM bytes."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_host import _build_c_example
+    from rtamd import render
+    nx, ny, spp = 64, 48, 4
+    exe = _build_c_example(tmp_path)
+    ppm_c = tmp_path / "c.ppm"
+    subprocess.run([str(exe), str(nx), str(ny), str(spp), str(ppm_c)], check=True, timeout=300)
+    acc = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.cornell_box(nx, ny), nx, ny, 0, spp, SEED, acc)
+    ppm_py = tmp_path / "py.ppm"
+    render.write_ppm(str(ppm_py), gpu.resolve_u8(acc, nx, ny, spp), nx, ny)
+    assert ppm_c.read_bytes() == ppm_py.read_bytes()

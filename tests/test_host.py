@@ -170,3 +170,21 @@ def test_medium_order_segments():
     assert [o.kind for o in sc.obj_list] == ["medium", "sphere"]
     with pytest.raises(ValueError):
         g.make_constant_medium(box, 0.0, g.constant_texture((1, 1, 1)))
+
+
+def _build_c_example(tmp_path):
+    import subprocess
+    exe = tmp_path / "cornell"
+    rtamd_dir = os.path.join(ROOT, "scheme-raytrace_amd", "rtamd")
+    subprocess.run(["gcc", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "cornell.c"), "-L", rtamd_dir, "-l:librtamd.so",
+                    "-Wl,-rpath," + rtamd_dir, "-o", str(exe)], check=True)
+    return exe
+
+
+def test_c_example_builds_against_the_abi(tmp_path):
+    """examples/cornell.c uses only include/rt.h and links librtamd.so."""
+    import subprocess
+    exe = _build_c_example(tmp_path)
+    out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
+    assert out.strip() == "rt_abi_version 2"
