@@ -28,6 +28,10 @@ hipError_t launch_shade(int, const DevScene&, const RenderParams&, const PathSta
 hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
                          unsigned long long*, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
+size_t extend_lds_bytes(const DevScene&);
+hipError_t extend_lds_prepare(size_t, uint32_t*);
+hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
+                             const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 }  // namespace rtamd
 
@@ -97,6 +101,9 @@ struct Scene {
     // flattened + uploaded
     DevScene dev{};
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
+    DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
+    size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
+    uint32_t ext_lds_blocks = 0;
     // render buffers
     DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
     uint32_t* h_counts = nullptr;     // pinned
@@ -388,6 +395,44 @@ double scene_radius(const Scene* s, const Flattener& f) {
     return 4 * R + 1;
 }
 
+// Build-time tree -> traversal layout (BvhNode2: both child boxes in the
+// parent, f32 rounded outward and widened by `margin`; child refs >= 0 inner,
+// < 0 ~leaf).  leaf_of(b, e) gives the BvhLeaf of a build leaf over refs
+// [b, e).  lane_stack = deepest BVH2 level (stack entries a traversal needs).
+template <class LeafFn>
+void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_of, std::vector<BvhNode2>& bvh2,
+                  std::vector<BvhLeaf>& bleaf, int32_t& root, int32_t& lane_stack) {
+    std::vector<int> inner_idx(nodes.size(), -1), leaf_idx(nodes.size(), -1);
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const BvhNode& N = nodes[i];
+        if (N.c == -1) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); continue; }
+        leaf_idx[i] = (int)bleaf.size();
+        bleaf.push_back(leaf_of(N.a, N.b));
+    }
+    auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        if (inner_idx[i] < 0) continue;
+        BvhNode2& M = bvh2[inner_idx[i]];
+        const BvhNode& L = nodes[nodes[i].a];
+        const BvhNode& R = nodes[nodes[i].b];
+        for (int k = 0; k < 3; ++k) {
+            M.lbox[k] = f32_down(L.lo[k] - margin); M.lbox[3 + k] = f32_up(L.hi[k] + margin);
+            M.rbox[k] = f32_down(R.lo[k] - margin); M.rbox[3 + k] = f32_up(R.hi[k] + margin);
+        }
+        M.l = ref_of(nodes[i].a); M.r = ref_of(nodes[i].b);
+    }
+    root = ref_of(0);
+    std::vector<int> depth(nodes.size(), 0);
+    for (size_t i = 0; i < nodes.size(); ++i)
+        if (nodes[i].c == -1) { depth[nodes[i].a] = depth[i] + 1; depth[nodes[i].b] = depth[i] + 1; }
+    for (int dd : depth) lane_stack = std::max(lane_stack, dd);
+}
+
+size_t extend_lds_budget() {     // RTAMD_EXTEND_LDS_MAX: largest LDS footprint k_extend_lds may take
+    const char* e = std::getenv("RTAMD_EXTEND_LDS_MAX");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)64 << 10;
+}
+
 int commit_scene(Scene* s, int world) {
     Context* c = get_ctx(s->ctx);
     if (!c) return fail("scene's context was destroyed");
@@ -480,6 +525,12 @@ int commit_scene(Scene* s, int world) {
     int32_t lane_stack = 0;
     bool bvh_has_bez = false;
     float bvh_pad = 0.0f;
+    double margin = 0.0;
+    std::vector<BvhNode2> fbvh2;                     // time-0 tree (see below)
+    std::vector<BvhLeaf> fbleaf;
+    std::vector<SphereRec> fsph;
+    std::vector<std::pair<int, int>> fsrc;           // (LEAF_SPHERE | LEAF_MSPHERE, local)
+    int32_t fbvh2_root = 0;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
@@ -494,40 +545,15 @@ int commit_scene(Scene* s, int world) {
         }
         bvh_has_bez = nb[refs.size()] > 0;
         bvh_nodes = std::move(bb.nodes);
-        // per-lane layout: child boxes in the parent
-        std::vector<int> inner_idx(bvh_nodes.size(), -1), leaf_idx(bvh_nodes.size(), -1);
-        for (size_t i = 0; i < bvh_nodes.size(); ++i) {
-            const BvhNode& N = bvh_nodes[i];
-            if (N.c == -1) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); continue; }
-            leaf_idx[i] = (int)bleaf.size();
-            const int b = N.a, e = N.b;
-            bleaf.push_back({ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0});
-        }
-        auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
         // f32 box margin: 2^-21 x a radius bound R on everything a ray can start
         // from (x4 included, see scene_radius).  The slab ends carry at most
         // ~4 ulps x (|box| + |o|) <= 2^-22 x 1.25 R of rounding; the margin is
         // 1.6x that.
-        const double margin = std::ldexp(scene_radius(s, f), -21);
+        margin = std::ldexp(scene_radius(s, f), -21);
         bvh_pad = (float)margin;
-        for (size_t i = 0; i < bvh_nodes.size(); ++i) {
-            if (inner_idx[i] < 0) continue;
-            BvhNode2& M = bvh2[inner_idx[i]];
-            const BvhNode& L = bvh_nodes[bvh_nodes[i].a];
-            const BvhNode& R = bvh_nodes[bvh_nodes[i].b];
-            for (int k = 0; k < 3; ++k) {
-                M.lbox[k] = f32_down(L.lo[k] - margin); M.lbox[3 + k] = f32_up(L.hi[k] + margin);
-                M.rbox[k] = f32_down(R.lo[k] - margin); M.rbox[3 + k] = f32_up(R.hi[k] + margin);
-            }
-            M.l = ref_of(bvh_nodes[i].a); M.r = ref_of(bvh_nodes[i].b);
-        }
-        bvh2_root = ref_of(0);
-
-        // stack entries a per-lane traversal can need = depth of the BVH2
-        std::vector<int> depth(bvh_nodes.size(), 0);
-        for (size_t i = 0; i < bvh_nodes.size(); ++i)
-            if (bvh_nodes[i].c == -1) { depth[bvh_nodes[i].a] = depth[i] + 1; depth[bvh_nodes[i].b] = depth[i] + 1; }
-        for (int dd : depth) lane_stack = std::max(lane_stack, dd);
+        flatten_bvh2(bvh_nodes, margin, [&](int b, int e) {
+            return BvhLeaf{ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0};
+        }, bvh2, bleaf, bvh2_root, lane_stack);
         const int gid = (int)groups.size();
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
@@ -554,6 +580,53 @@ int commit_scene(Scene* s, int world) {
                 bez.push_back(bezier_rec(o));
                 lbez.push_back(li);
             }
+        }
+        // Time-0 BVH.  Every scattered ray has time 0 (make-ray, ray.scm:8-9,
+        // Q4), so for those rays a moving sphere sits at center(0) exactly:
+        // the second tree bounds each moving sphere at that one position
+        // instead of over the whole shutter, and stores it as a plain sphere
+        // whose center is computed here with the kernel's own operations
+        // (c0 + dc * ((0 - t0) / den), IEEE f64, no contraction), so the
+        // primitive test it runs is bit-for-bit the moving-sphere test.
+        if (!bvh_has_bez && nm[refs.size()] > 0 && !std::getenv("RTAMD_NO_BVH0")) {
+            std::vector<PrimRef> refs0;
+            for (size_t i = 0; i < refs.size(); ++i) {
+                PrimRef r = refs[i];
+                r.leaf = (int)i;                     // index into refs (-> fsph / fid below)
+                if (r.type == LEAF_MSPHERE) {
+                    const MSphereRec& m = msph[(size_t)nm[i]];
+                    const double frac = (0.0 - m.t0) / m.den;
+                    const double c[3] = {m.c0x + m.dcx * frac, m.c0y + m.dcy * frac, m.c0z + m.dcz * frac};
+                    const double rad = std::sqrt(m.rr) * (1 + 1e-15) + 1e-300;
+                    const bool fin = std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]);
+                    for (int k = 0; k < 3; ++k) {
+                        r.lo[k] = fin ? c[k] - rad : -1e300;
+                        r.hi[k] = fin ? c[k] + rad : 1e300;
+                    }
+                    pad_box(r.lo, r.hi);
+                    for (int k = 0; k < 3; ++k) r.c[k] = 0.5 * (r.lo[k] + r.hi[k]);
+                }
+                refs0.push_back(r);
+            }
+            BvhBuild b0{refs0, {}};
+            b0.leaf_max = bb.leaf_max;
+            b0.trav_cost = bb.trav_cost;
+            b0.build(0, (int)refs0.size(), 0);
+            // fsph in refs0 order; each entry remembers which sphere / moving sphere it is
+            for (const PrimRef& r : refs0) {
+                const size_t i = (size_t)r.leaf;
+                if (r.type == LEAF_SPHERE) {
+                    fsph.push_back(sph[(size_t)ns[i]]);
+                    fsrc.push_back({LEAF_SPHERE, ns[i]});
+                } else {
+                    const MSphereRec& m = msph[(size_t)nm[i]];
+                    const double frac = (0.0 - m.t0) / m.den;
+                    fsph.push_back({m.c0x + m.dcx * frac, m.c0y + m.dcy * frac, m.c0z + m.dcz * frac, m.rr});
+                    fsrc.push_back({LEAF_MSPHERE, nm[i]});
+                }
+            }
+            flatten_bvh2(b0.nodes, margin, [&](int b, int e) { return BvhLeaf{b, e - b, 0, 0, 0, 0, 0, 0}; },
+                         fbvh2, fbleaf, fbvh2_root, lane_stack);
         }
     }
     std::vector<MediumRec> med;
@@ -695,6 +768,27 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
     d.n_bvh2 = (int)bvh2.size();
     d.bvh2_root = bvh2_root;
+    if (!fbvh2.empty()) {
+        std::vector<int32_t> fid;
+        for (const auto& sl : fsrc) fid.push_back(base[sl.first] + sl.second);
+        if (int rc = upload(s->d_fbvh2, fbvh2, &d.fbvh2)) return rc;
+        if (int rc = upload(s->d_fbleaf, fbleaf, &d.fbleaf)) return rc;
+        if (int rc = upload(s->d_fsph, fsph, &d.fsph)) return rc;
+        if (int rc = upload(s->d_fid, fid, &d.fid)) return rc;
+        d.fbvh2_root = fbvh2_root;
+        d.n_fbvh2 = (int)fbvh2.size(); d.n_fbleaf = (int)fbleaf.size(); d.n_fsph = (int)fsph.size();
+    }
+    s->ext_lds = 0;
+    s->ext_lds_blocks = 0;
+    if (!std::getenv("RTAMD_NO_EXTEND_LDS")) {
+        const size_t lds = extend_lds_bytes(d);
+        uint32_t mb = 0;
+        if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(lds, &mb) == hipSuccess && mb >= 256) {
+            s->ext_lds = lds;
+            s->ext_lds_blocks = mb;
+        }
+        (void)hipGetLastError();
+    }
     d.lane_stack = lane_stack;
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
@@ -876,7 +970,12 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             }
             uint32_t* cnt = s->counts.as<uint32_t>() + depth * kCountsPerIter;   // [class][shard], survivors at 4
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
-            HIPCHK(launch_extend(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt, stream));
+            if (depth > 0 && s->ext_lds)          // every ray of a depth >= 1 launch has time +0.0
+                HIPCHK(launch_extend_lds(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+                                         s->ext_lds_blocks, stream));
+            else
+                HIPCHK(launch_extend(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+                                     stream));
             if (s->profiling) HIPCHK(hipEventRecord(s->ev[1], stream));
             uint32_t* surv = cnt + 4 * kShards * kCntStride;
             for (int mt = 0; mt < 4; ++mt) {

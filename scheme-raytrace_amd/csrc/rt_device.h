@@ -114,6 +114,13 @@ struct DevScene {
     int32_t bvh_has_bez;                           // curves in the BVH: widen the box t range (see bvh_closest)
     float bvh_pad;                                 // the margin baked into the f32 boxes (diagnostic)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
+    // Time-0 tree over the same primitives (nullptr = none): every moving
+    // sphere frozen at center(0), so rays with time +0.0 (all scattered rays,
+    // Q4) traverse tighter boxes.  Leaves index fsph (plain sphere records in
+    // tree order); fid maps an fsph entry to its leaf id.
+    const BvhNode2* fbvh2; const BvhLeaf* fbleaf; int32_t fbvh2_root;
+    const SphereRec* fsph; const int32_t* fid;
+    int32_t n_fbvh2, n_fbleaf, n_fsph;
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
     int32_t leaf_base[kLeafTypes];             // first leaf id of each LeafType

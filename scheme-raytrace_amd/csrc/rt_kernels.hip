@@ -470,23 +470,54 @@ __device__ __forceinline__ bool box_hit_t(const float* bx, const BoxRay& r, cons
     return tnear <= tfar;
 }
 
+#ifdef RT_STATS
+// traversal statistics (stats builds only): rays, node visits, leaf visits,
+// sphere tests, moving-sphere tests, lane inner / outer loop iterations,
+// waves, wave-max inner / outer iterations, lanes; [0..10] all-times tree,
+// [16..26] time-0 tree
+__device__ unsigned long long g_stats[32];
+#define RT_STAT(k, v) atomicAdd(&g_stats[k], (unsigned long long)(v))
+#else
+#define RT_STAT(k, v) ((void)0)
+#endif
+
+// FROZEN: the time-0 tree (DevScene::fbvh2), whose leaves hold plain sphere
+// records (moving spheres at center(0)); otherwise the all-times tree.
+// nodes / leaves / fsph may point into LDS (k_extend_lds) or HBM.
+template <bool FROZEN>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
-                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax) {
+                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
+                                                 const BvhNode2* __restrict__ nodes,
+                                                 const BvhLeaf* __restrict__ leaves,
+                                                 const SphereRec* __restrict__ fsph) {
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d);
     const BoxRay br = box_ray(o, d);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
+    int32_t fbest = -1;                                       // FROZEN: fsph index of the best hit
     int sp = 0;
-    int32_t node = sc.bvh2_root, pend = kDone;
+    int32_t node = FROZEN ? sc.fbvh2_root : sc.bvh2_root, pend = kDone;
+#ifdef RT_STATS
+    uint32_t n_node = 0, n_leaf = 0, n_sph = 0, n_msph = 0, n_inner = 0, n_outer = 0;
+#endif
     while (node != kDone || pend != kDone) {
+#ifdef RT_STATS
+        ++n_outer;
+#endif
         while (node != kDone) {
+#ifdef RT_STATS
+            ++n_inner;
+#endif
             if (node < 0) {                                   // a leaf
                 if (pend != kDone) break;                     // one is already parked
                 pend = node;
                 node = sp ? (int32_t)lstk[--sp * stride] : kDone;
             } else {
-                const BvhNode2 N = sc.bvh2[node];
+#ifdef RT_STATS
+                ++n_node;
+#endif
+                const BvhNode2 N = nodes[node];
                 const float tcap = f32_up(closest);
                 float tl, tr;
                 const bool hl = box_hit_t(N.lbox, br, tcap, tl);
@@ -506,20 +537,57 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
         }
         if (pend != kDone) {
-            const BvhLeaf L = sc.bleaf[~pend];
-            for (int s = L.sb; s < L.sb + L.sn; ++s) {
-                const SphereRec S = sc.sph[s];
-                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
-            }
-            for (int s = L.mb; s < L.mb + L.mn; ++s) {
-                const MSphereRec S = sc.msph[s];
-                const double frac = (time - S.t0) / S.den;
-                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+            const BvhLeaf L = leaves[~pend];
+#ifdef RT_STATS
+            ++n_leaf;
+#endif
+            if (FROZEN) {
+                for (int s = L.sb; s < L.sb + L.sn; ++s) {
+#ifdef RT_STATS
+                    ++n_sph;
+#endif
+                    const SphereRec S = fsph[s];
+                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, s, closest, fbest);
+                }
+            } else {
+                for (int s = L.sb; s < L.sb + L.sn; ++s) {
+#ifdef RT_STATS
+                    ++n_sph;
+#endif
+                    const SphereRec S = sc.sph[s];
+                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                }
+                for (int s = L.mb; s < L.mb + L.mn; ++s) {
+#ifdef RT_STATS
+                    ++n_msph;
+#endif
+                    const MSphereRec S = sc.msph[s];
+                    const double frac = (time - S.t0) / S.den;
+                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                }
             }
             pend = kDone;
         }
     }
+    if (FROZEN && fbest >= 0) best = sc.fid[fbest];
+#ifdef RT_STATS
+    constexpr int so = FROZEN ? 16 : 0;
+    RT_STAT(so + 0, 1); RT_STAT(so + 1, n_node); RT_STAT(so + 2, n_leaf); RT_STAT(so + 3, n_sph);
+    RT_STAT(so + 4, n_msph); RT_STAT(so + 5, n_inner); RT_STAT(so + 6, n_outer);
+    {   // wave-level iterations: the wave runs until its slowest lane is done
+        const unsigned long long act = __ballot(1);
+        uint32_t mi = 0, mo = 0;
+        for (int l = 0; l < 64; ++l) {
+            if (!((act >> l) & 1ull)) continue;
+            mi = max(mi, (uint32_t)__builtin_amdgcn_readlane((int)n_inner, l));
+            mo = max(mo, (uint32_t)__builtin_amdgcn_readlane((int)n_outer, l));
+        }
+        if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)act) - 1)) {
+            RT_STAT(so + 7, 1); RT_STAT(so + 8, mi); RT_STAT(so + 9, mo); RT_STAT(so + 10, __popcll(act));
+        }
+    }
+#endif
 }
 
 // Per-lane traversal of a BVH that holds curves: spheres are tested on the
@@ -744,10 +812,14 @@ __device__ __forceinline__ bool medium_test(const DevScene& sc, const MediumRec&
     return true;
 }
 
+// The time-0 tree a kernel traverses (k_extend_lds stages it in LDS).
+struct Tree0 { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; };
+__device__ __forceinline__ Tree0 tree0_hbm(const DevScene& sc) { return Tree0{sc.fbvh2, sc.fbleaf, sc.fsph}; }
+
 template <int F>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
                                                const double time, double& closest, uint32_t* lstk,
-                                               const int lmax, BezWave* bw, Rng* rng) {
+                                               const int lmax, BezWave* bw, Rng* rng, const Tree0 t0) {
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     int32_t best = -1;
@@ -756,7 +828,9 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
         const Group G = sc.groups[g];
         if (G.type == GROUP_BVH) {
             if (BEZ && sc.bvh_has_bez) bvh_closest_curves(sc, o0, d0, time, closest, best, lstk, lmax, *bw);
-            else bvh_closest_lane(sc, o0, d0, time, closest, best, lstk, lmax);
+            else if (sc.fbvh2 && __double_as_longlong(time) == 0ll)    // time +0.0: the time-0 tree
+                bvh_closest_lane<true>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph);
+            else bvh_closest_lane<false>(sc, o0, d0, time, closest, best, lstk, lmax, sc.bvh2, sc.bleaf, nullptr);
             continue;
         }
         v3 o = o0, d = d0;
@@ -940,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         Rng g;
         if (MED) g.init(rp.k0, rp.k1, st.pix[i], st.smp[i], st.rng[i]);
         const int32_t leaf = closest_hit<F>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS,
-                                            &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g);
+                                            &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
         if (MED) st.rng[i] = g.ctr;                 // draws taken inside media
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
@@ -956,6 +1030,72 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     }
     const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
     if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+}
+
+// =====================================================================
+// k_extend_lds — k_extend for launches whose rays all carry time +0.0 (every
+// depth >= 1 launch) in scenes whose time-0 tree fits in LDS: persistent
+// blocks stage the tree (nodes, leaves, sphere records) into LDS once and
+// grid-stride over the queue, so node fetches cost LDS latency instead of
+// L1/L2 latency.  Sphere scenes only (no curves, media or Klein: F = 0).
+// =====================================================================
+#ifndef RT_EXTLDS_BLOCK
+#define RT_EXTLDS_BLOCK 512
+#endif
+#ifndef RT_EXTLDS_WAVES
+#define RT_EXTLDS_WAVES 6
+#endif
+constexpr int kExtLdsBlock = RT_EXTLDS_BLOCK;
+__global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(const DevScene sc, const RenderParams rp,
+                                                             const PathState st, const QView in, uint32_t n,
+                                                             HitBuf hit, uint32_t* __restrict__ queues,
+                                                             uint32_t qstride, uint32_t shard_cap,
+                                                             uint32_t* __restrict__ counts) {
+    extern __shared__ uint4 s_dyn[];
+    __shared__ uint32_t s_cnt[4 * 16 + 4];
+    const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
+    BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_dyn);
+    BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
+    SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
+    uint32_t* s_lstack = reinterpret_cast<uint32_t*>(s_sph + ns);
+    {   // stage the time-0 tree (16-B words, coalesced)
+        const uint4* g; uint4* l;
+        g = reinterpret_cast<const uint4*>(sc.fbvh2); l = reinterpret_cast<uint4*>(s_nodes);
+        for (int k = threadIdx.x; k < nn * 4; k += kExtLdsBlock) l[k] = g[k];
+        g = reinterpret_cast<const uint4*>(sc.fbleaf); l = reinterpret_cast<uint4*>(s_leaves);
+        for (int k = threadIdx.x; k < nl * 2; k += kExtLdsBlock) l[k] = g[k];
+        g = reinterpret_cast<const uint4*>(sc.fsph); l = reinterpret_cast<uint4*>(s_sph);
+        for (int k = threadIdx.x; k < ns * 2; k += kExtLdsBlock) l[k] = g[k];
+    }
+    __syncthreads();
+    const Tree0 t0{s_nodes, s_leaves, s_sph};
+    const int LS = sc.lane_stack;
+    const QMap qm = qmap(in);
+    for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
+        const uint32_t k = base + threadIdx.x;
+        int cls = -1;
+        uint32_t i = 0;
+        if (k < n) {
+            i = qphys(qm, k);
+            const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
+            const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
+            double t;
+            const int32_t leaf = closest_hit<0>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, nullptr, nullptr, t0);
+            if (leaf < 0) {
+                const v3 L = sky_radiance(sc, d);
+                const uint32_t wid = st.wid[i];
+                rp.sb[wid] = st.tr[i] * L.x;
+                rp.sb[rp.B + wid] = st.tg[i] * L.y;
+                rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+            } else {
+                hit.t[i] = t;
+                hit.leaf[i] = leaf;
+                cls = sc.mats[sc.leaves[leaf].mat].type;
+            }
+        }
+        const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
+        if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+    }
 }
 
 // ------------------------------------------------------------- textures
@@ -1321,7 +1461,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
             Rng g;
             if (MED) g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
             const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
-                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g);
+                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
             if (MED) p.rng = g.ctr;
             v3 L;
             bool cont = false;
@@ -1363,6 +1503,7 @@ __global__ __launch_bounds__(256) void k_resolve_u8(const double* __restrict__ a
 }
 
 // ------------------------------------------------------------ launchers
+#define HIP_RETURN_IF(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
 hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathState& st,
                          hipStream_t s) {
     const uint32_t blocks = (rp.B + 255u) / 256u;
@@ -1396,6 +1537,35 @@ hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathS
     }
 #undef RT_EXTEND_F
     return hipGetLastError();
+}
+// bytes of LDS k_extend_lds needs for the scene's time-0 tree (0 = cannot run)
+size_t extend_lds_bytes(const DevScene& sc) {
+    if (!sc.fbvh2 || sc.n_bez || sc.n_med || sc.n_klein) return 0;
+    return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+           (size_t)sc.n_fsph * sizeof(SphereRec) +
+           (size_t)kExtLdsBlock * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+}
+hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
+                             uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride,
+                             uint32_t shard_cap, uint32_t* counts, uint32_t max_blocks, hipStream_t s) {
+    const size_t lds = extend_lds_bytes(sc);
+    uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
+    if (blocks > max_blocks) blocks = max_blocks;
+    blocks = (blocks + kShards - 1) / kShards * kShards;      // every shard gets the same number of blocks
+    hipLaunchKernelGGL(k_extend_lds, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit, queues,
+                       qstride, shard_cap, counts);
+    return hipGetLastError();
+}
+// grid of k_extend_lds: every block it can keep resident on the device at once
+hipError_t extend_lds_prepare(size_t lds, uint32_t* max_blocks) {
+    HIP_RETURN_IF(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_extend_lds),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_RETURN_IF(hipGetDevice(&dev));
+    HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_lds, kExtLdsBlock, lds));
+    *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
+    return hipSuccess;
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
@@ -1432,6 +1602,16 @@ hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathS
 #undef RT_FINISH_F
     return hipGetLastError();
 }
+#ifdef RT_STATS
+extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof g_stats) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {
     const uint32_t blocks = (rp.npix + 255u) / 256u;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, s, rp, S, accum);

@@ -195,6 +195,51 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
+def _moving_mix_scene(nx, ny):
+    """Moving spheres whose shutters do not start at 0 (center(0) is an
+    extrapolation), a degenerate shutter (t0 = t1: center(0) is NaN, never
+    hit), static spheres, all three materials, and a camera shutter [0, 1]."""
+    from rtamd import scene as g, vec as v
+    from rtamd.rng import HostStream
+    rr = HostStream(0x5EED0101)
+    mats = [g.make_lambertian(g.constant_texture(v.vec3(0.5, 0.6, 0.7))),
+            g.make_metal(g.constant_texture(v.vec3(0.8, 0.7, 0.6)), 0.3), g.make_dielectric(1.5)]
+    objs = [g.make_sphere(v.vec3(0, -1000, 0), 1000, mats[0])]
+    for i in range(60):
+        c0 = v.vec3(rr() * 8 - 4, 0.2 + rr() * 0.5, rr() * 8 - 4)
+        c1 = v.sum(c0, v.vec3(rr() - 0.5, rr(), rr() - 0.5))
+        m = mats[i % 3]
+        if i % 4 == 0:
+            objs.append(g.make_sphere(c0, 0.25, m))
+        elif i % 4 == 1:
+            objs.append(g.make_moving_sphere(c0, c1, 0.5, 1.5, 0.2, m))
+        elif i % 4 == 2:
+            objs.append(g.make_moving_sphere(c0, c1, -1.0, 0.25, 0.3, m))
+        else:
+            objs.append(g.make_moving_sphere(c0, c1, 0.0, 1.0, 0.2, m))
+    objs.append(g.make_moving_sphere(v.vec3(0, 1, 0), v.vec3(0, 2, 0), 0.5, 0.5, 0.5, mats[0]))
+    return g.make_scene(objs, scenes.camera_for(nx, ny), g.sky_color)
+
+
+@pytest.mark.parametrize("make", [scenes.random_scene, _moving_mix_scene])
+def test_time0_bvh_matches_all_times_bvh_bitwise(gpu_ctx, monkeypatch, make):
+    """Scattered rays (time 0) traverse the time-0 tree with moving spheres
+    frozen at center(0); the image equals the one from the all-times tree and
+    the flat list bit for bit."""
+    nx, ny, spp = 64, 40, 4
+    imgs = []
+    for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_NO_BVH0": "1"}, {}):
+        for k in ("RTAMD_BVH_MIN", "RTAMD_NO_BVH0"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        a = np.zeros(nx * ny * 3)
+        gpu.render_host(make(nx, ny), nx, ny, 0, spp, SEED, a)
+        imgs.append(a)
+    assert np.array_equal(imgs[0], imgs[1])
+    assert np.array_equal(imgs[1], imgs[2])
+
+
 @pytest.mark.parametrize("name", ["test_scene", "test_scene2", "cornell", "cover", "bvh_sah", "test_bezier",
                                   "cornell_bezier", "cornell_smoke", "klein", "cornell_klein"])
 def test_gpu_vs_reference_fixtures(name, gpu_ctx):
