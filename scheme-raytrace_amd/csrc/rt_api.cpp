@@ -26,7 +26,7 @@ hipError_t launch_extend(const DevScene&, const RenderParams&, const PathState&,
 hipError_t launch_shade(int, const DevScene&, const RenderParams&, const PathState&, const HitBuf&,
                         const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, hipStream_t);
 hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         unsigned long long*, hipStream_t);
+                         unsigned long long*, size_t, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
 hipError_t extend_lds_prepare(size_t, uint32_t*);
@@ -84,6 +84,37 @@ struct Context {
     DevBuf accum_tmp, img_tmp;
 };
 
+// A lane = one path pool + stream.  render_impl deals the sample chunks of a
+// render to the lanes round-robin and keeps them in flight together, so the
+// long, narrow tail of one chunk (its last few paths bouncing to depth 100)
+// overlaps the wide first iterations of the next one instead of leaving the
+// chip mostly idle.  Accumulation stays in chunk (= sample) order.
+constexpr int kLanes = 2;
+struct Lane {
+    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, queues, seg_tail;
+    uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_cnt = nullptr;               // the last iteration's survivor counts are on the host
+    hipEvent_t ev_acc = nullptr;               // this lane's last accumulate
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};             // profiling: extend / shade brackets
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_fin;      // profiling: tail kernel brackets
+    size_t n_fin = 0;
+    // the chunk in flight
+    enum State { IDLE, RUNNING, DONE } state = IDLE;
+    int chunk = -1, depth = 0;
+    uint32_t n = 0, S = 0;
+    uint64_t seq = 0;                          // enqueue order of the pending iteration
+    RenderParams rp{};
+    PathState A{}, B{}, *cur = nullptr, *nxt = nullptr;
+    QView view{nullptr, 0};
+    ~Lane() {
+        if (h_counts) (void)hipHostFree(h_counts);
+        for (hipEvent_t e : {ev_cnt, ev_acc, ev[0], ev[1], ev[2]}) if (e) (void)hipEventDestroy(e);
+        for (auto& pr : ev_fin) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
 struct Scene {
     int ctx = -1;
     std::vector<DevTexture> texs;
@@ -104,19 +135,13 @@ struct Scene {
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
     uint32_t ext_lds_blocks = 0;
-    // render buffers
-    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, pixlist, queues, seg_tail;
-    uint32_t* h_counts = nullptr;     // pinned
+    // render buffers: one path pool per lane (render_impl)
+    DevBuf pixlist;
+    std::unique_ptr<Lane> lanes[kLanes];
     int pix_nx = -1, pix_ny = -1, pix_shard = -1, pix_nshard = -1;
     uint32_t pix_n = 0;
     bool profiling = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     rt_stats stats{};
-
-    ~Scene() {
-        if (h_counts) (void)hipHostFree(h_counts);
-        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
-    }
 };
 
 std::mutex g_mu;
@@ -851,8 +876,18 @@ std::vector<uint32_t> make_pixlist(int nx, int ny, int shard, int nshard) {
 
 size_t max_paths() {
     const char* e = std::getenv("RTAMD_MAX_PATHS");
-    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)32 << 20;
+    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)64 << 20;
     return v < 1024 ? 1024 : v;
+}
+
+int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = no overlap)
+    const char* e = std::getenv("RTAMD_LANES");
+    return e ? std::max(1, std::atoi(e)) : kLanes;
+}
+
+bool debug_counts() {
+    static const bool v = std::getenv("RTAMD_DEBUG_COUNTS") != nullptr;
+    return v;
 }
 
 uint32_t tail_threshold() {
@@ -861,7 +896,7 @@ uint32_t tail_threshold() {
 }
 uint32_t tail_divisor() {
     const char* e = std::getenv("RTAMD_TAIL_DIV");
-    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 32ul;
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 64ul;
     return v ? (uint32_t)v : 1u;
 }
 
@@ -904,6 +939,8 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     const size_t cap_paths = max_paths();
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
+    const int nchunks = (int)((spp_count + chunk - 1) / chunk);
+    const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_wanted()), nchunks));
     const size_t cap = (size_t)npix * chunk;
     // sharded compaction (rt_device.h kShards): shard capacity bounds what the
     // blocks of one shard can append in one wavefront step (extend: one item
@@ -912,107 +949,197 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     const size_t shard_cap = (cap + kShards - 1) / kShards + 4 * 32 * gmax + 256;
     const size_t scap = shard_cap * kShards;
     if (scap >= (1ull << 32)) return fail("path pool too large");
-    HIPCHK(s->st_a.ensure(scap * kStateBytesPerPath));
-    HIPCHK(s->st_b.ensure(scap * kStateBytesPerPath));
-    HIPCHK(s->hit_t.ensure(scap * sizeof(double)));
-    HIPCHK(s->hit_leaf.ensure(scap * sizeof(int32_t)));
-    HIPCHK(s->sb.ensure(cap * 3 * sizeof(double)));
     constexpr int kCountsPerIter = 5 * kShards * kCntStride;   // 4 material queues + survivors, 8 shards each
     constexpr int kIters = kMaxDepth + 4;
-    HIPCHK(s->counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
-    HIPCHK(s->queues.ensure(scap * 4 * sizeof(uint32_t)));
-    HIPCHK(s->seg_tail.ensure(2 * sizeof(unsigned long long)));   // tail segments, next tail path
-    HIPCHK(hipMemsetAsync(s->seg_tail.p, 0, 2 * sizeof(unsigned long long), stream));
-    if (!s->h_counts) HIPCHK(hipHostMalloc((void**)&s->h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
-    if (s->profiling && !s->ev[0])
-        for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
-
-    PathState A = carve_state(s->st_a.p, scap), Bst = carve_state(s->st_b.p, scap);
-    HitBuf hit{s->hit_t.as<double>(), s->hit_leaf.as<int32_t>()};
+    // callers' prior work on `stream` (e.g. zeroing accum) comes first
+    hipEvent_t ev_in = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    std::unique_ptr<void, void (*)(void*)> ev_in_guard(ev_in, [](void* e) { (void)hipEventDestroy((hipEvent_t)e); });
+    HIPCHK(hipEventRecord(ev_in, stream));
+    for (int li = 0; li < nlanes; ++li) {
+        if (!s->lanes[li]) s->lanes[li].reset(new Lane());
+        Lane& L = *s->lanes[li];
+        if (!L.stream) HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+        if (!L.ev_cnt) HIPCHK(hipEventCreateWithFlags(&L.ev_cnt, hipEventDisableTiming));
+        if (!L.ev_acc) HIPCHK(hipEventCreateWithFlags(&L.ev_acc, hipEventDisableTiming));
+        if (s->profiling && !L.ev[0]) for (auto& e : L.ev) HIPCHK(hipEventCreate(&e));
+        HIPCHK(L.st_a.ensure(scap * kStateBytesPerPath));
+        HIPCHK(L.st_b.ensure(scap * kStateBytesPerPath));
+        HIPCHK(L.hit_t.ensure(scap * sizeof(double)));
+        HIPCHK(L.hit_leaf.ensure(scap * sizeof(int32_t)));
+        HIPCHK(L.sb.ensure(cap * 3 * sizeof(double)));
+        HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
+        HIPCHK(L.queues.ensure(scap * 4 * sizeof(uint32_t)));
+        HIPCHK(L.seg_tail.ensure(2 * sizeof(unsigned long long)));   // tail segments, next tail path
+        if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
+        HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
+        HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 2 * sizeof(unsigned long long), L.stream));
+        L.A = carve_state(L.st_a.p, scap);
+        L.B = carve_state(L.st_b.p, scap);
+        L.state = Lane::IDLE;
+        L.n_fin = 0;
+    }
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    uint32_t* queues = s->queues.as<uint32_t>();
     const uint32_t qstride = (uint32_t)scap;
     const int mat_mask = s->dev.mat_mask;
+    uint64_t seq = 0;
 
-    for (int done = 0; done < spp_count; done += (int)chunk) {
-        const uint32_t S = (uint32_t)std::min<int>((int)chunk, spp_count - done);
-        RenderParams rp{};
+    // Enqueue the lane's next step for its current path count: one wavefront
+    // iteration (extend + shades + the survivor-count readback), or, below
+    // the tail threshold, the tail kernel that finishes every remaining path.
+    auto step = [&](Lane& L) -> int {
+        const uint32_t tail = std::max<uint32_t>(tail_threshold(), L.rp.B / tail_divisor());
+        if (L.n == 0) { L.state = Lane::DONE; return 0; }
+        if (L.depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
+        if (L.n <= tail) {
+            std::pair<hipEvent_t, hipEvent_t>* fe = nullptr;
+            if (s->profiling) {
+                if (L.n_fin == L.ev_fin.size()) {
+                    hipEvent_t e0 = nullptr, e1 = nullptr;
+                    HIPCHK(hipEventCreate(&e0));
+                    HIPCHK(hipEventCreate(&e1));
+                    L.ev_fin.push_back({e0, e1});
+                }
+                fe = &L.ev_fin[L.n_fin++];
+                HIPCHK(hipEventRecord(fe->first, L.stream));
+            }
+            HIPCHK(hipMemsetAsync(L.seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), L.stream));
+            HIPCHK(launch_finish(s->dev, L.rp, *L.cur, L.view, L.n, L.seg_tail.as<unsigned long long>(),
+                                 s->ext_lds ? (size_t)32 << 10 : 0, L.stream));
+            if (fe) HIPCHK(hipEventRecord(fe->second, L.stream));
+            s->stats.finish_paths += L.n;
+            L.state = Lane::DONE;
+            return 0;
+        }
+        uint32_t* cnt = L.counts.as<uint32_t>() + L.depth * kCountsPerIter;   // [class][shard], survivors at 4
+        HitBuf hit{L.hit_t.as<double>(), L.hit_leaf.as<int32_t>()};
+        uint32_t* queues = L.queues.as<uint32_t>();
+        if (s->profiling) HIPCHK(hipEventRecord(L.ev[0], L.stream));
+        if (L.depth > 0 && s->ext_lds)          // every ray of a depth >= 1 launch has time +0.0
+            HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap,
+                                     cnt, s->ext_lds_blocks, L.stream));
+        else
+            HIPCHK(launch_extend(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+                                 L.stream));
+        if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
+        uint32_t* surv = cnt + 4 * kShards * kCntStride;
+        for (int mt = 0; mt < 4; ++mt) {
+            if (!(mat_mask & (1 << mt))) continue;
+            const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
+            HIPCHK(launch_shade(mt, s->dev, L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
+                                (uint32_t)shard_cap, L.stream));
+        }
+        if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));
+        HIPCHK(hipMemcpyAsync(L.h_counts + L.depth * kCountsPerIter, surv, kShards * kCntStride * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, L.stream));
+        HIPCHK(hipEventRecord(L.ev_cnt, L.stream));
+        L.state = Lane::RUNNING;
+        L.seq = seq++;
+        return 0;
+    };
+    // The iteration's counts have arrived: take its statistics, move on.
+    auto advance = [&](Lane& L) -> int {
+        if (s->profiling) {
+            float a = 0, b = 0;
+            HIPCHK(hipEventElapsedTime(&a, L.ev[0], L.ev[1]));
+            HIPCHK(hipEventElapsedTime(&b, L.ev[1], L.ev[2]));
+            s->stats.ms_extend += a; s->stats.ms_shade += b;
+            s->stats.extend_launches += 1;
+        }
+        s->stats.extend_rays += L.n;
+        s->stats.segments += L.n;
+        if ((uint32_t)L.depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)L.depth;
+        uint32_t n = 0;
+        for (int x = 0; x < kShards; ++x) {
+            const uint32_t c_x = L.h_counts[L.depth * kCountsPerIter + x * kCntStride];
+            if (c_x > shard_cap) return fail("internal: shard overflow");
+            n += c_x;
+        }
+        L.view = QView{L.counts.as<uint32_t>() + L.depth * kCountsPerIter + 4 * kShards * kCntStride,
+                       (uint32_t)shard_cap};
+        std::swap(L.cur, L.nxt);
+        L.n = n;
+        ++L.depth;
+        if (debug_counts() && L.chunk == 0) std::fprintf(stderr, "rtamd: chunk 0 depth %d paths %u\n", L.depth, n);
+        return step(L);
+    };
+    auto start = [&](Lane& L, int ch) -> int {
+        const int done = ch * (int)chunk;
+        L.chunk = ch;
+        L.S = (uint32_t)std::min<int>((int)chunk, spp_count - done);
+        RenderParams& rp = L.rp;
+        rp = RenderParams{};
         rp.nx = (uint32_t)nx; rp.ny = (uint32_t)ny; rp.npix = npix;
         rp.spp0 = (uint32_t)(spp_begin + done); rp.k0 = k0; rp.k1 = k1;
         rp.pixlist = s->pixlist.as<const uint32_t>();
-        rp.sb = s->sb.as<double>();
-        rp.B = npix * S;
-        // below the tail threshold one k_finish launch completes every
-        // remaining path (extend + shade looped per thread)
-        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / tail_divisor());
-        HIPCHK(hipMemsetAsync(s->counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), stream));
-        HIPCHK(launch_raygen(s->dev, rp, A, stream));
-        PathState* cur = &A;
-        PathState* nxt = &Bst;
-        QView view{nullptr, (uint32_t)scap};         // raygen output: contiguous
-        uint32_t n = rp.B;
+        rp.sb = L.sb.as<double>();
+        rp.B = npix * L.S;
+        HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
+        HIPCHK(launch_raygen(s->dev, rp, L.A, L.stream));
+        L.cur = &L.A;
+        L.nxt = &L.B;
+        L.view = QView{nullptr, (uint32_t)scap};         // raygen output: contiguous
+        L.n = rp.B;
+        L.depth = 0;
         s->stats.paths += rp.B;
-        for (int depth = 0; n > 0; ++depth) {
-            if (depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
-            if (n <= tail) {
-                if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
-                HIPCHK(hipMemsetAsync(s->seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), stream));
-                HIPCHK(launch_finish(s->dev, rp, *cur, view, n, s->seg_tail.as<unsigned long long>(), stream));
-                if (s->profiling) {
-                    HIPCHK(hipEventRecord(s->ev[1], stream));
-                    HIPCHK(hipEventSynchronize(s->ev[1]));
-                    float a = 0;
-                    HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
-                    s->stats.ms_finish += a;
-                }
-                s->stats.finish_paths += n;
-                break;
-            }
-            uint32_t* cnt = s->counts.as<uint32_t>() + depth * kCountsPerIter;   // [class][shard], survivors at 4
-            if (s->profiling) HIPCHK(hipEventRecord(s->ev[0], stream));
-            if (depth > 0 && s->ext_lds)          // every ray of a depth >= 1 launch has time +0.0
-                HIPCHK(launch_extend_lds(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
-                                         s->ext_lds_blocks, stream));
-            else
-                HIPCHK(launch_extend(s->dev, rp, *cur, view, n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
-                                     stream));
-            if (s->profiling) HIPCHK(hipEventRecord(s->ev[1], stream));
-            uint32_t* surv = cnt + 4 * kShards * kCntStride;
-            for (int mt = 0; mt < 4; ++mt) {
-                if (!(mat_mask & (1 << mt))) continue;
-                const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
-                HIPCHK(launch_shade(mt, s->dev, rp, *cur, hit, queues + (size_t)mt * qstride, qv, n, *nxt, surv,
-                                    (uint32_t)shard_cap, stream));
-            }
-            if (s->profiling) HIPCHK(hipEventRecord(s->ev[2], stream));
-            HIPCHK(hipMemcpyAsync(s->h_counts + depth * kCountsPerIter, surv, kShards * kCntStride * sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipStreamSynchronize(stream));
-            if (s->profiling) {
-                float a = 0, b = 0;
-                HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
-                HIPCHK(hipEventElapsedTime(&b, s->ev[1], s->ev[2]));
-                s->stats.ms_extend += a; s->stats.ms_shade += b;
-                s->stats.extend_launches += 1;
-            }
-            s->stats.extend_rays += n;
-            s->stats.segments += n;
-            if ((uint32_t)depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)depth;
-            n = 0;
-            for (int x = 0; x < kShards; ++x) {
-                const uint32_t c_x = s->h_counts[depth * kCountsPerIter + x * kCntStride];
-                if (c_x > shard_cap) return fail("internal: shard overflow");
-                n += c_x;
-            }
-            view = QView{surv, (uint32_t)shard_cap};
-            std::swap(cur, nxt);
+        if (debug_counts() && ch == 0) std::fprintf(stderr, "rtamd: chunk 0 depth 0 paths %u\n", L.n);
+        return step(L);
+    };
+
+    int next_chunk = 0, next_acc = 0;
+    Lane* last_acc = nullptr;
+    while (next_acc < nchunks) {
+        bool progressed = false;
+        for (int li = 0; li < nlanes; ++li) {           // accumulate in chunk order
+            Lane& L = *s->lanes[li];
+            if (L.state != Lane::DONE || L.chunk != next_acc) continue;
+            if (last_acc && last_acc != &L) HIPCHK(hipStreamWaitEvent(L.stream, last_acc->ev_acc, 0));
+            HIPCHK(launch_accumulate(L.rp, L.S, accum, L.stream));
+            HIPCHK(hipEventRecord(L.ev_acc, L.stream));
+            last_acc = &L;
+            ++next_acc;
+            L.state = Lane::IDLE;
+            progressed = true;
+            li = -1;                                     // the next chunk may sit on an earlier lane
         }
-        HIPCHK(launch_accumulate(rp, S, accum, stream));
+        for (int li = 0; li < nlanes; ++li) {           // idle lanes take the next chunk
+            Lane& L = *s->lanes[li];
+            if (L.state != Lane::IDLE || next_chunk >= nchunks) continue;
+            if (int rc = start(L, next_chunk++)) return rc;
+            progressed = true;
+        }
+        for (int li = 0; li < nlanes; ++li) {           // lanes whose counts have arrived
+            Lane& L = *s->lanes[li];
+            if (L.state != Lane::RUNNING) continue;
+            const hipError_t q = hipEventQuery(L.ev_cnt);
+            if (q == hipErrorNotReady) continue;
+            HIPCHK(q);
+            if (int rc = advance(L)) return rc;
+            progressed = true;
+        }
+        if (progressed) continue;
+        Lane* oldest = nullptr;                          // nothing to do: wait for the oldest pending step
+        for (int li = 0; li < nlanes; ++li) {
+            Lane& L = *s->lanes[li];
+            if (L.state == Lane::RUNNING && (!oldest || L.seq < oldest->seq)) oldest = &L;
+        }
+        if (!oldest) return fail("internal: render lanes stalled");
+        HIPCHK(hipEventSynchronize(oldest->ev_cnt));
     }
+    for (int li = 0; li < nlanes; ++li) HIPCHK(hipStreamSynchronize(s->lanes[li]->stream));
+    for (int li = 0; li < nlanes; ++li) {
+        Lane& L = *s->lanes[li];
+        unsigned long long tail_segs = 0;
+        HIPCHK(hipMemcpy(&tail_segs, L.seg_tail.p, sizeof tail_segs, hipMemcpyDeviceToHost));
+        s->stats.segments += tail_segs;
+        for (size_t k = 0; k < L.n_fin; ++k) {
+            float a = 0;
+            HIPCHK(hipEventElapsedTime(&a, L.ev_fin[k].first, L.ev_fin[k].second));
+            s->stats.ms_finish += a;
+        }
+    }
+    // later work on the caller's stream sees the finished accumulator
     HIPCHK(hipStreamSynchronize(stream));
-    unsigned long long tail_segs = 0;
-    HIPCHK(hipMemcpy(&tail_segs, s->seg_tail.p, sizeof tail_segs, hipMemcpyDeviceToHost));
-    s->stats.segments += tail_segs;
     s->stats.ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return 0;

@@ -1139,6 +1139,33 @@ __device__ __forceinline__ double perlin_turb(const PerlinLds& P, v3 p) {       
     }
     return fabs(acc);
 }
+// checker-texture's test (texture.scm:16-23): (< (* (sin 10x) (sin 10y)
+// (sin 10z)) 0).  Only the product's sign matters, so each factor's sign is
+// found by reducing y = 10x to r = y - k*pi (k = rint(y/pi), three-part pi,
+// fma: |error| < 1e-14 for |y| < 2^20): sin y = (-1)^k sin r.  When every |r|
+// exceeds 1e-12 the signs are certain, no factor is 0 and the product (above
+// 1e-37) cannot underflow, so the test equals the one on libm / OCML sines;
+// otherwise (near a zero, huge or NaN arguments) the sines are evaluated.
+__device__ __forceinline__ bool sin_sign_neg(const double y, bool& sure) {
+    constexpr double kInvPi = 0.31830988618379067154;
+    constexpr double kPiA = 3.1415926218032836914;               // pi split in three (Cody-Waite)
+    constexpr double kPiB = 3.1786509424591713469e-08;
+    constexpr double kPiC = 1.2246467864107188502e-16;
+    const double k = rint(y * kInvPi);
+    const double r = fma(-k, kPiC, fma(-k, kPiB, fma(-k, kPiA, y)));
+    sure = sure && fabs(y) < 1048576.0 && fabs(r) > 1e-12;
+    const bool odd = ((long long)k & 1ll) != 0;
+    return odd != (r < 0.0);
+}
+__device__ __forceinline__ bool checker_odd(const v3 p) {
+    const double x = 10.0 * p.x, y = 10.0 * p.y, z = 10.0 * p.z;
+    bool sure = true;
+    const bool nx = sin_sign_neg(x, sure), ny = sin_sign_neg(y, sure), nz = sin_sign_neg(z, sure);
+    if (sure) return (nx != ny) != nz;
+    const double sines = sin(x) * sin(y) * sin(z);
+    return sines < 0.0;
+}
+
 // PN = false compiles the noise / marble cases out (scenes without them)
 template <bool PN>
 __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, int id, v3 p) {   // texture.scm
@@ -1146,8 +1173,7 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
         const DevTexture t = sc.texs[id];
         if (t.type == TEX_CONSTANT) return mk(t.r, t.g, t.bl);
         if (t.type == TEX_CHECKER) {                                 // :16-23
-            const double sines = sin(10.0 * p.x) * sin(10.0 * p.y) * sin(10.0 * p.z);
-            id = (sines < 0.0) ? t.b : t.a;
+            id = checker_odd(p) ? t.b : t.a;
             continue;
         }
         if (!PN) return mk(0.0, 0.0, 0.0);
@@ -1422,13 +1448,33 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 template <int F>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
-                                                unsigned long long* __restrict__ tail_ctl) {
+                                                unsigned long long* __restrict__ tail_ctl, int tree0_lds) {
     __shared__ PerlinLds P;
-    extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
+    // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
+    // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in k_extend_lds
+    extern __shared__ uint4 s_fdyn[];
+    uint32_t* s_lstack = reinterpret_cast<uint32_t*>(s_fdyn);
     const int LS = sc.lane_stack;
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
+    Tree0 t0 = tree0_hbm(sc);
+    if (tree0_lds) {
+        const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
+        const int words = (256 * (LS > 0 ? LS : 1) + 3) / 4;           // stack size in uint4
+        BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_fdyn + words);
+        BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
+        SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
+        const uint4* g; uint4* l;
+        g = reinterpret_cast<const uint4*>(sc.fbvh2); l = reinterpret_cast<uint4*>(s_nodes);
+        for (int k = threadIdx.x; k < nn * 4; k += 256) l[k] = g[k];
+        g = reinterpret_cast<const uint4*>(sc.fbleaf); l = reinterpret_cast<uint4*>(s_leaves);
+        for (int k = threadIdx.x; k < nl * 2; k += 256) l[k] = g[k];
+        g = reinterpret_cast<const uint4*>(sc.fsph); l = reinterpret_cast<uint4*>(s_sph);
+        for (int k = threadIdx.x; k < ns * 2; k += 256) l[k] = g[k];
+        t0 = Tree0{s_nodes, s_leaves, s_sph};
+        __syncthreads();
+    }
     stage_perlin(sc, P);
     // Persistent lanes: a lane whose path ended takes the next unstarted one
     // (one atomic per wave per refill), so a wave is not held by its longest
@@ -1461,7 +1507,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
             Rng g;
             if (MED) g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
             const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
-                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
+                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, t0);
             if (MED) p.rng = g.ctr;
             v3 L;
             bool cont = false;
@@ -1587,12 +1633,16 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
     return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
-                         uint32_t n, unsigned long long* seg_count, hipStream_t s) {
+                         uint32_t n, unsigned long long* seg_count, size_t tree0_budget, hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
     if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
-    const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+    size_t lds = ((size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t) + 15) / 16 * 16;
+    const size_t tree = (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+                        (size_t)sc.n_fsph * sizeof(SphereRec);
+    const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
+    if (tree0_lds) lds += tree;
 #define RT_FINISH_F(F) \
-    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count)
+    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count, tree0_lds)
     switch (scene_features(sc)) {
     case 0: RT_FINISH_F(0); break;
     case 1: RT_FINISH_F(1); break;

@@ -105,6 +105,22 @@ def test_batching_independent_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("lanes", ["1", "2"])
+def test_lanes_and_chunks_bitwise(gpu_ctx, monkeypatch, lanes):
+    """Overlapped path pools (lanes) and many small chunks give the one-chunk
+    image bit for bit: chunks are accumulated in sample order whichever lane
+    finishes first."""
+    nx, ny, spp = 48, 40, 12
+    scene = scenes.random_scene(nx, ny)
+    a = np.zeros(nx * ny * 3)
+    gpu.render_host(scene, nx, ny, 0, spp, SEED, a)
+    monkeypatch.setenv("RTAMD_MAX_PATHS", str(nx * ny * 2))   # 6 chunks of 2 spp
+    monkeypatch.setenv("RTAMD_LANES", lanes)
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(scene, nx, ny, 0, spp, SEED, b)
+    assert np.array_equal(a, b)
+
+
 def test_shards_union_bitwise(gpu_ctx):
     """Interleaved tile shards (the multi-GPU partition) reassemble the
     single-device image bit for bit."""

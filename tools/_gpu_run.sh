@@ -4,7 +4,8 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/pytest_gpu.log
 run() { tag=$1; shift; env "$@" timeout -k 10 300 python bench.py --spp 256 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_$tag.log 2>&1 || exit 1
   python -c "import json,sys; d=json.loads(open('gpurun_out/bench_$tag.log').read().strip().splitlines()[-1]); print('$tag', d['value'], d['ms_per_step'], d['ms_extend_per_step'], d['ms_shade_per_step'], d['ms_finish_per_step'])"; }
-run lds_w6 X=1
-run nolds RTAMD_NO_EXTEND_LDS=1
-run lds_w1 RTAMD_LIB=scheme-raytrace_amd/rtamd/librtamd_w1.so
-run lds_b256 RTAMD_LIB=scheme-raytrace_amd/rtamd/librtamd_b256.so
+run lanes2 X=1
+run lanes1 RTAMD_LANES=1
+run lanes2_32M RTAMD_MAX_PATHS=33554432
+run lanes2_noprof X=1
+run lanes2_div64 RTAMD_TAIL_DIV=64
