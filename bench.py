@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile-events", action="store_true")
+    p.add_argument("--no-isolated", action="store_true", help="skip the single-lane profiling frame")
     return p.parse_args()
 
 
@@ -153,6 +154,17 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # One more (untimed) frame with a single render lane: the overlapped lanes
+    # of the timed steps run two chunks' kernels concurrently, so a kernel's
+    # event-bracketed duration there includes its neighbour's work.  This
+    # frame gives each kernel's duration with the chip to itself.
+    iso = None
+    if not a.no_profile_events and not a.no_isolated:
+        os.environ["RTAMD_LANES"] = "1"
+        try:
+            iso = step()
+        finally:
+            del os.environ["RTAMD_LANES"]
     tot = torch.tensor([segs, paths], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -164,6 +176,16 @@ def main():
         value = segs_all / elapsed / 1e6
         roof = None
         valu = None
+        roof_iso = None
+        if iso is not None and iso.extend_launches and iso.ms_extend > 0:
+            bpl = extend_bytes(iso.extend_rays, iso.paths) / iso.extend_launches
+            ams = iso.ms_extend / iso.extend_launches
+            ach = bpl / (ams * 1e-3) / 1e9
+            roof_iso = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": "k_extend + k_extend_lds",
+                        "bytes_per_launch": round(bpl), "rays_per_launch": round(iso.extend_rays / iso.extend_launches),
+                        "avg_launch_ms": round(ams, 4),
+                        "note": "one extra untimed frame with a single render lane (no concurrent kernels)"}
         if launches and ms_ext > 0:
             # wavefront extend launches only (the depth tail runs in k_finish)
             wf_segs = segs - tail_segs
@@ -183,8 +205,9 @@ def main():
                 traffic = round(pm["bytes_per_segment"] * rays_per_launch)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "k_extend", "bytes_per_launch": round(bytes_per_launch),
-                    "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4)}
+                    "kernel": "k_extend + k_extend_lds", "bytes_per_launch": round(bytes_per_launch),
+                    "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4),
+                    "note": "timed region; render lanes overlap, so launch durations include concurrent kernels"}
             if pm and pm.get("f64_flops_per_segment"):
                 tf = pm["f64_flops_per_segment"] * rays_per_launch / (avg_ms * 1e-3) / 1e12
                 valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
@@ -200,7 +223,7 @@ def main():
                                    % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp),
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
-            "roofline": roof, "valu": valu,
+            "roofline": roof, "roofline_isolated": roof_iso, "valu": valu,
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),

@@ -22,11 +22,12 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, hipStream_t);
+                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const RenderParams&, const PathState&, const HitBuf&,
-                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, hipStream_t);
+                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, bool,
+                        hipStream_t);
 hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         unsigned long long*, size_t, hipStream_t);
+                         unsigned long long*, size_t, bool, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
 hipError_t extend_lds_prepare(size_t, uint32_t*);
@@ -900,7 +901,7 @@ uint32_t tail_divisor() {
     return v ? (uint32_t)v : 1u;
 }
 
-constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 5 * sizeof(uint32_t);
+constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 3 * sizeof(uint32_t);
 
 PathState carve_state(void* base, size_t cap) {
     PathState st;
@@ -908,7 +909,7 @@ PathState carve_state(void* base, size_t cap) {
     st.ox = dp; st.oy = dp + cap; st.oz = dp + 2 * cap; st.dx = dp + 3 * cap; st.dy = dp + 4 * cap;
     st.dz = dp + 5 * cap; st.tm = dp + 6 * cap; st.tr = dp + 7 * cap; st.tg = dp + 8 * cap; st.tb = dp + 9 * cap;
     uint32_t* up = reinterpret_cast<uint32_t*>(dp + 10 * cap);
-    st.pix = up; st.smp = up + cap; st.wid = up + 2 * cap; st.rng = up + 3 * cap; st.depth = up + 4 * cap;
+    st.wid = up; st.rng = up + cap; st.depth = up + 2 * cap;
     return st;
 }
 
@@ -1005,7 +1006,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             }
             HIPCHK(hipMemsetAsync(L.seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), L.stream));
             HIPCHK(launch_finish(s->dev, L.rp, *L.cur, L.view, L.n, L.seg_tail.as<unsigned long long>(),
-                                 s->ext_lds ? (size_t)32 << 10 : 0, L.stream));
+                                 s->ext_lds ? (size_t)32 << 10 : 0, L.depth == 0, L.stream));
             if (fe) HIPCHK(hipEventRecord(fe->second, L.stream));
             s->stats.finish_paths += L.n;
             L.state = Lane::DONE;
@@ -1020,14 +1021,14 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
                                      cnt, s->ext_lds_blocks, L.stream));
         else
             HIPCHK(launch_extend(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
-                                 L.stream));
+                                 L.depth == 0, L.stream));
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
         for (int mt = 0; mt < 4; ++mt) {
             if (!(mat_mask & (1 << mt))) continue;
             const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
             HIPCHK(launch_shade(mt, s->dev, L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
-                                (uint32_t)shard_cap, L.stream));
+                                (uint32_t)shard_cap, L.depth == 0, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));
         HIPCHK(hipMemcpyAsync(L.h_counts + L.depth * kCountsPerIter, surv, kShards * kCntStride * sizeof(uint32_t),

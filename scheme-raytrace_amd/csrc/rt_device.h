@@ -137,10 +137,15 @@ struct DevScene {
 };
 
 // Wavefront path state, SoA, one slot per live path (ping-pong buffers).
+// A path's pixel and absolute sample index follow from its work id (wid =
+// s_rel * npix + q: pixel pixlist[q], sample spp0 + s_rel), so they are not
+// stored.  Depth-0 state (raygen output) holds only what varies per camera
+// ray — o, d, time, draw counter (throughput is 1, wid is the slot, depth 0);
+// scattered rays all have time 0 (Q4), so deeper state has no time.
 struct PathState {
-    double *ox, *oy, *oz, *dx, *dy, *dz, *tm;   // ray
-    double *tr, *tg, *tb;                        // throughput
-    uint32_t *pix, *smp, *wid, *rng, *depth;     // pixel, absolute sample, work id, draw counter, depth
+    double *ox, *oy, *oz, *dx, *dy, *dz, *tm;   // ray (tm: depth-0 state only)
+    double *tr, *tg, *tb;                        // throughput (depth >= 1)
+    uint32_t *wid, *rng, *depth;                 // work id, draw counter, depth (wid, depth: depth >= 1)
 };
 struct HitBuf { double* t; int32_t* leaf; };
 

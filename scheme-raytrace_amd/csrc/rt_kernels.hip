@@ -146,11 +146,10 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
     const v3 o = origin + offset;
     const v3 d = ((mk(c.llc[0], c.llc[1], c.llc[2]) + mk(c.hor[0], c.hor[1], c.hor[2]) * u) +
                   mk(c.ver[0], c.ver[1], c.ver[2]) * v) - origin - offset;
-    st.ox[w] = o.x; st.oy[w] = o.y; st.oz[w] = o.z;
+    st.ox[w] = o.x; st.oy[w] = o.y; st.oz[w] = o.z;      // depth-0 state (rt_device.h PathState)
     st.dx[w] = d.x; st.dy[w] = d.y; st.dz[w] = d.z;
     st.tm[w] = time;
-    st.tr[w] = 1.0; st.tg[w] = 1.0; st.tb[w] = 1.0;
-    st.pix[w] = j; st.smp[w] = smp; st.wid[w] = w; st.rng[w] = g.ctr; st.depth[w] = 0u;
+    st.rng[w] = g.ctr;
 }
 
 // ---------------------------------------------------------- closest hit
@@ -904,19 +903,35 @@ struct PathRegs {
     v3 T;
     uint32_t pix, smp, wid, rng, depth;
 };
-__device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathRegs& p) {
+// pixel and absolute sample of work id wid (RNG keys, see PathState)
+__device__ __forceinline__ void wid_key(const RenderParams& rp, const uint32_t wid, uint32_t& pix, uint32_t& smp) {
+    const uint32_t s_rel = wid / rp.npix;
+    pix = rp.pixlist[wid - s_rel * rp.npix];
+    smp = rp.spp0 + s_rel;
+}
+// depth0: slot i of the raygen output (wid = i, throughput 1, depth 0)
+__device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathRegs& p, const RenderParams& rp,
+                                          const bool depth0) {
     p.o = mk(st.ox[i], st.oy[i], st.oz[i]);
     p.d = mk(st.dx[i], st.dy[i], st.dz[i]);
-    p.time = st.tm[i];
-    p.T = mk(st.tr[i], st.tg[i], st.tb[i]);
-    p.pix = st.pix[i]; p.smp = st.smp[i]; p.wid = st.wid[i]; p.rng = st.rng[i]; p.depth = st.depth[i];
+    p.rng = st.rng[i];
+    if (depth0) {
+        p.time = st.tm[i];
+        p.T = mk(1.0, 1.0, 1.0);
+        p.wid = i; p.depth = 0u;
+    } else {
+        p.time = 0.0;                                    // every scattered ray (Q4)
+        p.T = mk(st.tr[i], st.tg[i], st.tb[i]);
+        p.wid = st.wid[i]; p.depth = st.depth[i];
+    }
+    wid_key(rp, p.wid, p.pix, p.smp);
 }
+// a scattered path (depth >= 1: no time)
 __device__ __forceinline__ void store_path(const PathState& st, uint32_t k, const PathRegs& p) {
     st.ox[k] = p.o.x; st.oy[k] = p.o.y; st.oz[k] = p.o.z;
     st.dx[k] = p.d.x; st.dy[k] = p.d.y; st.dz[k] = p.d.z;
-    st.tm[k] = p.time;
     st.tr[k] = p.T.x; st.tg[k] = p.T.y; st.tb[k] = p.T.z;
-    st.pix[k] = p.pix; st.smp[k] = p.smp; st.wid[k] = p.wid; st.rng[k] = p.rng; st.depth[k] = p.depth;
+    st.wid[k] = p.wid; st.rng[k] = p.rng; st.depth[k] = p.depth;
 }
 // path done: sample colour = T (*) L into the chunk's sample buffer
 __device__ __forceinline__ void write_sample(const RenderParams& rp, const PathRegs& p, const v3 L) {
@@ -996,7 +1011,8 @@ template <int F>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                 uint32_t* __restrict__ queues, uint32_t qstride,
-                                                uint32_t shard_cap, uint32_t* __restrict__ counts) {
+                                                uint32_t shard_cap, uint32_t* __restrict__ counts,
+                                                const bool depth0) {
     extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
     const int LS = sc.lane_stack;
     __shared__ uint32_t s_cnt[4 * 16 + 4];
@@ -1012,16 +1028,26 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
         double t;
         Rng g;
-        if (MED) g.init(rp.k0, rp.k1, st.pix[i], st.smp[i], st.rng[i]);
-        const int32_t leaf = closest_hit<F>(sc, o, d, st.tm[i], t, s_lstack + threadIdx.x, LS,
+        if (MED) {
+            uint32_t pix, smp;
+            wid_key(rp, depth0 ? i : st.wid[i], pix, smp);
+            g.init(rp.k0, rp.k1, pix, smp, st.rng[i]);
+        }
+        const int32_t leaf = closest_hit<F>(sc, o, d, depth0 ? st.tm[i] : 0.0, t, s_lstack + threadIdx.x, LS,
                                             &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
         if (MED) st.rng[i] = g.ctr;                 // draws taken inside media
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
-            const uint32_t wid = st.wid[i];
-            rp.sb[wid] = st.tr[i] * L.x;
-            rp.sb[rp.B + wid] = st.tg[i] * L.y;
-            rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+            if (depth0) {                                // throughput 1: (* 1 x) = x
+                rp.sb[i] = 1.0 * L.x;
+                rp.sb[rp.B + i] = 1.0 * L.y;
+                rp.sb[2u * rp.B + i] = 1.0 * L.z;
+            } else {
+                const uint32_t wid = st.wid[i];
+                rp.sb[wid] = st.tr[i] * L.x;
+                rp.sb[rp.B + wid] = st.tg[i] * L.y;
+                rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+            }
         } else {
             hit.t[i] = t;
             hit.leaf[i] = leaf;
@@ -1413,10 +1439,13 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 // k_shade<MAT> — one material's queue; survivors compacted into `out`
 // =====================================================================
 template <int MAT, bool PN>
-__global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderParams rp, const PathState in,
+#ifndef RT_SHADE_WAVES
+#define RT_SHADE_WAVES 1
+#endif
+__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene sc, const RenderParams rp, const PathState in,
                                                const HitBuf hit, const uint32_t* __restrict__ queue,
                                                const QView qv, PathState out, uint32_t* __restrict__ out_counts,
-                                               uint32_t shard_cap) {
+                                               uint32_t shard_cap, const bool depth0) {
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
     stage_perlin<PN>(sc, P);
@@ -1430,7 +1459,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
         PathRegs p;
         if (k < n) {
             const uint32_t i = queue[qphys(qm, k)];
-            load_path(in, i, p);
+            load_path(in, i, p, rp, depth0);
             v3 L;
             alive = shade_hit<MAT, PN>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
             if (!alive) write_sample(rp, p, L);
@@ -1448,7 +1477,8 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene sc, const RenderPa
 template <int F>
 __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
-                                                unsigned long long* __restrict__ tail_ctl, int tree0_lds) {
+                                                unsigned long long* __restrict__ tail_ctl, int tree0_lds,
+                                                const bool depth0) {
     __shared__ PerlinLds P;
     // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
     // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in k_extend_lds
@@ -1497,7 +1527,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderP
             if (base + cnt >= n) exhausted = true;
             if (!active) {
                 const uint32_t k = base + lanes_below(need);
-                if (k < n) { load_path(st, qphys(qm, k), p); active = true; }
+                if (k < n) { load_path(st, qphys(qm, k), p, rp, depth0); active = true; }
             }
         }
         if (__ballot(active) == 0ull) break;
@@ -1569,12 +1599,12 @@ static int scene_features(const DevScene& sc) {
 }
 hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
-                         uint32_t* counts, hipStream_t s) {
+                         uint32_t* counts, bool depth0, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
 #define RT_EXTEND_F(F)                                                                                      \
     hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit, queues,     \
-                       qstride, shard_cap, counts)
+                       qstride, shard_cap, counts, depth0)
     switch (scene_features(sc)) {
     case 0: RT_EXTEND_F(0); break;
     case 1: RT_EXTEND_F(1); break;
@@ -1615,13 +1645,14 @@ hipError_t extend_lds_prepare(size_t lds, uint32_t* max_blocks) {
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
-                        const PathState& out, uint32_t* out_counts, uint32_t shard_cap, hipStream_t s) {
+                        const PathState& out, uint32_t* out_counts, uint32_t shard_cap, bool depth0, hipStream_t s) {
     uint32_t blocks = (n_upper + 255u) / 256u;
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > 4096u) blocks = 4096u;
     if (blocks == 0u) blocks = kShards;
 #define RT_SHADE(M, PN) \
-    hipLaunchKernelGGL((k_shade<M, PN>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, shard_cap)
+    hipLaunchKernelGGL((k_shade<M, PN>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, \
+                       shard_cap, depth0)
     const bool pn = sc.has_noise_tex != 0;
     switch (mat) {
     case MAT_LAMBERTIAN: if (pn) RT_SHADE(MAT_LAMBERTIAN, true); else RT_SHADE(MAT_LAMBERTIAN, false); break;
@@ -1633,7 +1664,8 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
     return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
-                         uint32_t n, unsigned long long* seg_count, size_t tree0_budget, hipStream_t s) {
+                         uint32_t n, unsigned long long* seg_count, size_t tree0_budget, bool depth0,
+                         hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
     if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
     size_t lds = ((size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t) + 15) / 16 * 16;
@@ -1642,7 +1674,7 @@ hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathS
     const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
     if (tree0_lds) lds += tree;
 #define RT_FINISH_F(F) \
-    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count, tree0_lds)
+    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count, tree0_lds, depth0)
     switch (scene_features(sc)) {
     case 0: RT_FINISH_F(0); break;
     case 1: RT_FINISH_F(1); break;
