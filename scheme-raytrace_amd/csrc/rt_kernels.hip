@@ -1282,7 +1282,9 @@ __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g
 // queue holds (compile-time; -1 = any, used by the tail kernel).  Returns true
 // if the path continues (p holds the scattered ray, new throughput, depth+1);
 // otherwise L is the terminal radiance (emission or 0).
-template <int MATF, bool PN = true>
+// LS = false compiles the light-sampling mixture (f2) out: scenes without a
+// light target never take it, and its constants cost scalar registers.
+template <int MATF, bool PN = true, bool LS = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
                                           PathRegs& p, const double t, const int32_t leaf, v3& L) {
     L = mk(0.0, 0.0, 0.0);
@@ -1324,7 +1326,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     if (!can_continue) return false;                         // depth cap (main.scm:112,119)
     Rng g;
     g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
-    if (mt == MAT_LAMBERTIAN && sc.light.type != LIGHT_OFF) {
+    if (LS && mt == MAT_LAMBERTIAN && sc.light.type != LIGHT_OFF) {
         // pdf.scm mixture of (hitable-pdf light p) and (cosine-pdf normal)
         // (extension f2; oracle: rt_oracle.c light_pdf_value / light_random)
         const v3 axis2 = unit(nrm);
@@ -1438,7 +1440,7 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 // =====================================================================
 // k_shade<MAT> — one material's queue; survivors compacted into `out`
 // =====================================================================
-template <int MAT, bool PN>
+template <int MAT, bool PN, bool LS>
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 1
 #endif
@@ -1461,7 +1463,7 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene sc
             const uint32_t i = queue[qphys(qm, k)];
             load_path(in, i, p, rp, depth0);
             v3 L;
-            alive = shade_hit<MAT, PN>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
+            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
@@ -1650,15 +1652,19 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > 4096u) blocks = 4096u;
     if (blocks == 0u) blocks = kShards;
-#define RT_SHADE(M, PN) \
-    hipLaunchKernelGGL((k_shade<M, PN>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, out_counts, \
-                       shard_cap, depth0)
+#define RT_SHADE(M, PN, LS) \
+    hipLaunchKernelGGL((k_shade<M, PN, LS>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, \
+                       out_counts, shard_cap, depth0)
     const bool pn = sc.has_noise_tex != 0;
+    const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
     switch (mat) {
-    case MAT_LAMBERTIAN: if (pn) RT_SHADE(MAT_LAMBERTIAN, true); else RT_SHADE(MAT_LAMBERTIAN, false); break;
-    case MAT_METAL: if (pn) RT_SHADE(MAT_METAL, true); else RT_SHADE(MAT_METAL, false); break;
-    case MAT_DIELECTRIC: RT_SHADE(MAT_DIELECTRIC, false); break;          // attenuation is constant 1
-    default: if (pn) RT_SHADE(MAT_DIFFUSE_LIGHT, true); else RT_SHADE(MAT_DIFFUSE_LIGHT, false); break;
+    case MAT_LAMBERTIAN:
+        if (ls) { if (pn) RT_SHADE(MAT_LAMBERTIAN, true, true); else RT_SHADE(MAT_LAMBERTIAN, false, true); }
+        else { if (pn) RT_SHADE(MAT_LAMBERTIAN, true, false); else RT_SHADE(MAT_LAMBERTIAN, false, false); }
+        break;
+    case MAT_METAL: if (pn) RT_SHADE(MAT_METAL, true, false); else RT_SHADE(MAT_METAL, false, false); break;
+    case MAT_DIELECTRIC: RT_SHADE(MAT_DIELECTRIC, false, false); break;          // attenuation is constant 1
+    default: if (pn) RT_SHADE(MAT_DIFFUSE_LIGHT, true, false); else RT_SHADE(MAT_DIFFUSE_LIGHT, false, false); break;
     }
 #undef RT_SHADE
     return hipGetLastError();
