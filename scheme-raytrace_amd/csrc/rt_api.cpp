@@ -23,7 +23,7 @@ namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
                          const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, hipStream_t);
-hipError_t launch_shade(int, const DevScene&, const RenderParams&, const PathState&, const HitBuf&,
+hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, bool,
                         hipStream_t);
 hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
@@ -92,7 +92,7 @@ struct Context {
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
 constexpr int kLanes = 2;
 struct Lane {
-    DevBuf st_a, st_b, hit_t, hit_leaf, sb, counts, queues, seg_tail;
+    DevBuf st_a, st_b, hit, sb, counts, queues, seg_tail;
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
     hipStream_t stream = nullptr;
     hipEvent_t ev_cnt = nullptr;               // the last iteration's survivor counts are on the host
@@ -134,6 +134,7 @@ struct Scene {
     DevScene dev{};
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
+    DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
     uint32_t ext_lds_blocks = 0;
     // render buffers: one path pool per lane (render_impl)
@@ -855,6 +856,8 @@ int commit_scene(Scene* s, int world) {
     d.cam.lens = cm[21]; d.cam.t0 = cm[22]; d.cam.t1 = cm[23];
     for (const Obj& o : s->objs)
         if (o.mat >= (int)s->mats.size()) return fail("object refers to an unknown material");
+    HIPCHK(s->d_dev.ensure(sizeof(DevScene)));
+    HIPCHK(hipMemcpy(s->d_dev.p, &d, sizeof(DevScene), hipMemcpyHostToDevice));
     s->committed = true;
     return 0;
 }
@@ -901,15 +904,18 @@ uint32_t tail_divisor() {
     return v ? (uint32_t)v : 1u;
 }
 
-constexpr size_t kStateBytesPerPath = 10 * sizeof(double) + 3 * sizeof(uint32_t);
+constexpr size_t kStateBytesPerPath = sizeof(RayRec) + sizeof(PathRec) + sizeof(double) + sizeof(uint32_t);
 
 PathState carve_state(void* base, size_t cap) {
     PathState st;
-    double* dp = static_cast<double*>(base);
-    st.ox = dp; st.oy = dp + cap; st.oz = dp + 2 * cap; st.dx = dp + 3 * cap; st.dy = dp + 4 * cap;
-    st.dz = dp + 5 * cap; st.tm = dp + 6 * cap; st.tr = dp + 7 * cap; st.tg = dp + 8 * cap; st.tb = dp + 9 * cap;
-    uint32_t* up = reinterpret_cast<uint32_t*>(dp + 10 * cap);
-    st.wid = up; st.rng = up + cap; st.depth = up + 2 * cap;
+    char* p = static_cast<char*>(base);
+    st.ray = reinterpret_cast<RayRec*>(p);
+    p += cap * sizeof(RayRec);
+    st.path = reinterpret_cast<PathRec*>(p);
+    p += cap * sizeof(PathRec);
+    st.tm = reinterpret_cast<double*>(p);
+    p += cap * sizeof(double);
+    st.rng0 = reinterpret_cast<uint32_t*>(p);
     return st;
 }
 
@@ -966,8 +972,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         if (s->profiling && !L.ev[0]) for (auto& e : L.ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(L.st_a.ensure(scap * kStateBytesPerPath));
         HIPCHK(L.st_b.ensure(scap * kStateBytesPerPath));
-        HIPCHK(L.hit_t.ensure(scap * sizeof(double)));
-        HIPCHK(L.hit_leaf.ensure(scap * sizeof(int32_t)));
+        HIPCHK(L.hit.ensure(scap * sizeof(HitRec)));
         HIPCHK(L.sb.ensure(cap * 3 * sizeof(double)));
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(L.queues.ensure(scap * 4 * sizeof(uint32_t)));
@@ -1013,7 +1018,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             return 0;
         }
         uint32_t* cnt = L.counts.as<uint32_t>() + L.depth * kCountsPerIter;   // [class][shard], survivors at 4
-        HitBuf hit{L.hit_t.as<double>(), L.hit_leaf.as<int32_t>()};
+        HitBuf hit{L.hit.as<HitRec>()};
         uint32_t* queues = L.queues.as<uint32_t>();
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[0], L.stream));
         if (L.depth > 0 && s->ext_lds)          // every ray of a depth >= 1 launch has time +0.0
@@ -1027,7 +1032,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         for (int mt = 0; mt < 4; ++mt) {
             if (!(mat_mask & (1 << mt))) continue;
             const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
-            HIPCHK(launch_shade(mt, s->dev, L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
+            HIPCHK(launch_shade(mt, s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
                                 (uint32_t)shard_cap, L.depth == 0, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));

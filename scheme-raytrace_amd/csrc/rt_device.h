@@ -142,12 +142,18 @@ struct DevScene {
 // stored.  Depth-0 state (raygen output) holds only what varies per camera
 // ray — o, d, time, draw counter (throughput is 1, wid is the slot, depth 0);
 // scattered rays all have time 0 (Q4), so deeper state has no time.
+// Records, not one array per field: a lane reads its ray with three 16-B
+// loads, and a kernel holds 4 base pointers instead of 13 (scalar registers).
+struct alignas(16) RayRec { double ox, oy, oz, dx, dy, dz; };                 // 48 B
+struct alignas(8) PathRec { double tr, tg, tb; uint32_t wid, rng, depth, pad; };   // 40 B, depth >= 1
 struct PathState {
-    double *ox, *oy, *oz, *dx, *dy, *dz, *tm;   // ray (tm: depth-0 state only)
-    double *tr, *tg, *tb;                        // throughput (depth >= 1)
-    uint32_t *wid, *rng, *depth;                 // work id, draw counter, depth (wid, depth: depth >= 1)
+    RayRec* ray;          // origin, direction
+    PathRec* path;        // depth >= 1: throughput, work id, draw counter, depth
+    double* tm;           // depth 0: time
+    uint32_t* rng0;       // depth 0: draw counter
 };
-struct HitBuf { double* t; int32_t* leaf; };
+struct alignas(16) HitRec { double t; int32_t leaf, pad; };
+struct HitBuf { HitRec* h; };
 
 // Sharded queues.  Stream compaction appends through one atomic per block
 // and class on a counter chosen by blockIdx % kShards (8 XCDs), so no single

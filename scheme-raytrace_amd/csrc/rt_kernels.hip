@@ -146,10 +146,9 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
     const v3 o = origin + offset;
     const v3 d = ((mk(c.llc[0], c.llc[1], c.llc[2]) + mk(c.hor[0], c.hor[1], c.hor[2]) * u) +
                   mk(c.ver[0], c.ver[1], c.ver[2]) * v) - origin - offset;
-    st.ox[w] = o.x; st.oy[w] = o.y; st.oz[w] = o.z;      // depth-0 state (rt_device.h PathState)
-    st.dx[w] = d.x; st.dy[w] = d.y; st.dz[w] = d.z;
+    st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};      // depth-0 state (rt_device.h PathState)
     st.tm[w] = time;
-    st.rng[w] = g.ctr;
+    st.rng0[w] = g.ctr;
 }
 
 // ---------------------------------------------------------- closest hit
@@ -912,26 +911,25 @@ __device__ __forceinline__ void wid_key(const RenderParams& rp, const uint32_t w
 // depth0: slot i of the raygen output (wid = i, throughput 1, depth 0)
 __device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathRegs& p, const RenderParams& rp,
                                           const bool depth0) {
-    p.o = mk(st.ox[i], st.oy[i], st.oz[i]);
-    p.d = mk(st.dx[i], st.dy[i], st.dz[i]);
-    p.rng = st.rng[i];
+    const RayRec R = st.ray[i];
+    p.o = mk(R.ox, R.oy, R.oz);
+    p.d = mk(R.dx, R.dy, R.dz);
     if (depth0) {
         p.time = st.tm[i];
         p.T = mk(1.0, 1.0, 1.0);
-        p.wid = i; p.depth = 0u;
+        p.wid = i; p.depth = 0u; p.rng = st.rng0[i];
     } else {
+        const PathRec P = st.path[i];
         p.time = 0.0;                                    // every scattered ray (Q4)
-        p.T = mk(st.tr[i], st.tg[i], st.tb[i]);
-        p.wid = st.wid[i]; p.depth = st.depth[i];
+        p.T = mk(P.tr, P.tg, P.tb);
+        p.wid = P.wid; p.depth = P.depth; p.rng = P.rng;
     }
     wid_key(rp, p.wid, p.pix, p.smp);
 }
 // a scattered path (depth >= 1: no time)
 __device__ __forceinline__ void store_path(const PathState& st, uint32_t k, const PathRegs& p) {
-    st.ox[k] = p.o.x; st.oy[k] = p.o.y; st.oz[k] = p.o.z;
-    st.dx[k] = p.d.x; st.dy[k] = p.d.y; st.dz[k] = p.d.z;
-    st.tr[k] = p.T.x; st.tg[k] = p.T.y; st.tb[k] = p.T.z;
-    st.wid[k] = p.wid; st.rng[k] = p.rng; st.depth[k] = p.depth;
+    st.ray[k] = RayRec{p.o.x, p.o.y, p.o.z, p.d.x, p.d.y, p.d.z};
+    st.path[k] = PathRec{p.T.x, p.T.y, p.T.z, p.wid, p.rng, p.depth, 0u};
 }
 // path done: sample colour = T (*) L into the chunk's sample buffer
 __device__ __forceinline__ void write_sample(const RenderParams& rp, const PathRegs& p, const v3 L) {
@@ -1024,18 +1022,21 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     uint32_t i = 0;
     if (k < n) {
         i = qphys(qmap(in), k);
-        const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
-        const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
+        const RayRec R = st.ray[i];
+        const v3 o = mk(R.ox, R.oy, R.oz);
+        const v3 d = mk(R.dx, R.dy, R.dz);
         double t;
         Rng g;
         if (MED) {
             uint32_t pix, smp;
-            wid_key(rp, depth0 ? i : st.wid[i], pix, smp);
-            g.init(rp.k0, rp.k1, pix, smp, st.rng[i]);
+            wid_key(rp, depth0 ? i : st.path[i].wid, pix, smp);
+            g.init(rp.k0, rp.k1, pix, smp, depth0 ? st.rng0[i] : st.path[i].rng);
         }
         const int32_t leaf = closest_hit<F>(sc, o, d, depth0 ? st.tm[i] : 0.0, t, s_lstack + threadIdx.x, LS,
                                             &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
-        if (MED) st.rng[i] = g.ctr;                 // draws taken inside media
+        if (MED) {                                   // draws taken inside media
+            if (depth0) st.rng0[i] = g.ctr; else st.path[i].rng = g.ctr;
+        }
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             if (depth0) {                                // throughput 1: (* 1 x) = x
@@ -1043,14 +1044,13 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
                 rp.sb[rp.B + i] = 1.0 * L.y;
                 rp.sb[2u * rp.B + i] = 1.0 * L.z;
             } else {
-                const uint32_t wid = st.wid[i];
-                rp.sb[wid] = st.tr[i] * L.x;
-                rp.sb[rp.B + wid] = st.tg[i] * L.y;
-                rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+                const PathRec P = st.path[i];
+                rp.sb[P.wid] = P.tr * L.x;
+                rp.sb[rp.B + P.wid] = P.tg * L.y;
+                rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
             }
         } else {
-            hit.t[i] = t;
-            hit.leaf[i] = leaf;
+            hit.h[i] = HitRec{t, leaf, 0};
             cls = sc.mats[sc.leaves[leaf].mat].type;
         }
     }
@@ -1103,19 +1103,19 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
         uint32_t i = 0;
         if (k < n) {
             i = qphys(qm, k);
-            const v3 o = mk(st.ox[i], st.oy[i], st.oz[i]);
-            const v3 d = mk(st.dx[i], st.dy[i], st.dz[i]);
+            const RayRec R = st.ray[i];
+            const v3 o = mk(R.ox, R.oy, R.oz);
+            const v3 d = mk(R.dx, R.dy, R.dz);
             double t;
             const int32_t leaf = closest_hit<0>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, nullptr, nullptr, t0);
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);
-                const uint32_t wid = st.wid[i];
-                rp.sb[wid] = st.tr[i] * L.x;
-                rp.sb[rp.B + wid] = st.tg[i] * L.y;
-                rp.sb[2u * rp.B + wid] = st.tb[i] * L.z;
+                const PathRec P = st.path[i];
+                rp.sb[P.wid] = P.tr * L.x;
+                rp.sb[rp.B + P.wid] = P.tg * L.y;
+                rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
             } else {
-                hit.t[i] = t;
-                hit.leaf[i] = leaf;
+                hit.h[i] = HitRec{t, leaf, 0};
                 cls = sc.mats[sc.leaves[leaf].mat].type;
             }
         }
@@ -1444,10 +1444,11 @@ template <int MAT, bool PN, bool LS>
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 1
 #endif
-__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene sc, const RenderParams rp, const PathState in,
+__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp, const PathState in,
                                                const HitBuf hit, const uint32_t* __restrict__ queue,
                                                const QView qv, PathState out, uint32_t* __restrict__ out_counts,
                                                uint32_t shard_cap, const bool depth0) {
+    const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
     stage_perlin<PN>(sc, P);
@@ -1463,7 +1464,8 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene sc
             const uint32_t i = queue[qphys(qm, k)];
             load_path(in, i, p, rp, depth0);
             v3 L;
-            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, hit.t[i], hit.leaf[i], L);
+            const HitRec H = hit.h[i];
+            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
@@ -1645,7 +1647,7 @@ hipError_t extend_lds_prepare(size_t lds, uint32_t* max_blocks) {
     *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
     return hipSuccess;
 }
-hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, const PathState& in,
+hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
                         const PathState& out, uint32_t* out_counts, uint32_t shard_cap, bool depth0, hipStream_t s) {
     uint32_t blocks = (n_upper + 255u) / 256u;
@@ -1653,7 +1655,7 @@ hipError_t launch_shade(int mat, const DevScene& sc, const RenderParams& rp, con
     if (blocks > 4096u) blocks = 4096u;
     if (blocks == 0u) blocks = kShards;
 #define RT_SHADE(M, PN, LS) \
-    hipLaunchKernelGGL((k_shade<M, PN, LS>), dim3(blocks), dim3(256), 0, s, sc, rp, in, hit, queue, qv, out, \
+    hipLaunchKernelGGL((k_shade<M, PN, LS>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hit, queue, qv, out, \
                        out_counts, shard_cap, depth0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
