@@ -21,12 +21,12 @@
 
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
-hipError_t launch_extend(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
+hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
                          const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, bool,
                         hipStream_t);
-hipError_t launch_finish(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
+hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
                          unsigned long long*, size_t, bool, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
@@ -443,8 +443,8 @@ void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_
         const BvhNode& L = nodes[nodes[i].a];
         const BvhNode& R = nodes[nodes[i].b];
         for (int k = 0; k < 3; ++k) {
-            M.lbox[k] = f32_down(L.lo[k] - margin); M.lbox[3 + k] = f32_up(L.hi[k] + margin);
-            M.rbox[k] = f32_down(R.lo[k] - margin); M.rbox[3 + k] = f32_up(R.hi[k] + margin);
+            M.b[2 * k] = f32_down(L.lo[k] - margin); M.b[6 + 2 * k] = f32_up(L.hi[k] + margin);
+            M.b[2 * k + 1] = f32_down(R.lo[k] - margin); M.b[7 + 2 * k] = f32_up(R.hi[k] + margin);
         }
         M.l = ref_of(nodes[i].a); M.r = ref_of(nodes[i].b);
     }
@@ -560,6 +560,9 @@ int commit_scene(Scene* s, int world) {
     int32_t fbvh2_root = 0;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
+        // sphere trees: one primitive per leaf (measured fastest); curve trees keep 2
+        bb.leaf_max = std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; })
+                          ? 2 : 1;
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("RTAMD_BVH_CT")) bb.trav_cost = std::atof(e);
         bb.build(0, (int)refs.size(), 0);
@@ -1010,7 +1013,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
                 HIPCHK(hipEventRecord(fe->first, L.stream));
             }
             HIPCHK(hipMemsetAsync(L.seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), L.stream));
-            HIPCHK(launch_finish(s->dev, L.rp, *L.cur, L.view, L.n, L.seg_tail.as<unsigned long long>(),
+            HIPCHK(launch_finish(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, L.seg_tail.as<unsigned long long>(),
                                  s->ext_lds ? (size_t)32 << 10 : 0, L.depth == 0, L.stream));
             if (fe) HIPCHK(hipEventRecord(fe->second, L.stream));
             s->stats.finish_paths += L.n;
@@ -1025,7 +1028,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap,
                                      cnt, s->ext_lds_blocks, L.stream));
         else
-            HIPCHK(launch_extend(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+            HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
                                  L.depth == 0, L.stream));
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;

@@ -67,7 +67,10 @@ struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density,
 // absolute margin that covers the f32 slab test's rounding for any ray whose
 // origin lies within the scene's radius (see commit_scene), so culling stays
 // conservative.
-struct alignas(64) BvhNode2 { float lbox[6]; float rbox[6]; int32_t l, r, pad0, pad1; };
+// Child boxes interleaved left/right per plane, b = {lx0, rx0, ly0, ry0, lz0,
+// rz0, lx1, rx1, ly1, ry1, lz1, rz1}: the kernel tests both children with
+// packed f32 FMAs (v_pk_fma_f32) on adjacent register pairs.
+struct alignas(64) BvhNode2 { float b[12]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
 constexpr int kLaneStack = 32;                 // max per-lane traversal stack (dynamic LDS, stride = block size)
 

@@ -459,13 +459,21 @@ __device__ __forceinline__ BoxRay box_ray(const v3 o, const v3 d) {
     b.px = (float)(o.x * ix); b.py = (float)(o.y * iy); b.pz = (float)(o.z * iz);
     return b;
 }
-__device__ __forceinline__ bool box_hit_t(const float* bx, const BoxRay& r, const float tcap, float& tnear) {
-    const float tx0 = fmaf(bx[0], r.ix, -r.px), tx1 = fmaf(bx[3], r.ix, -r.px);
-    const float ty0 = fmaf(bx[1], r.iy, -r.py), ty1 = fmaf(bx[4], r.iy, -r.py);
-    const float tz0 = fmaf(bx[2], r.iz, -r.pz), tz1 = fmaf(bx[5], r.iz, -r.pz);
-    tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
-    return tnear <= tfar;
+// Both child boxes of N (interleaved planes, BvhNode2): slab ends t = fma(box,
+// 1/d, -o/d), near / far per child; hit iff near <= far.  (Packed v_pk_fma_f32
+// pairs were measured slower here: the pairs raise register pressure.)
+__device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, const float tcap, bool& hl, bool& hr,
+                                         float& tl, float& tr) {
+    auto one = [&](const int c, float& tn) {
+        const float tx0 = fmaf(N.b[0 + c], r.ix, -r.px), tx1 = fmaf(N.b[6 + c], r.ix, -r.px);
+        const float ty0 = fmaf(N.b[2 + c], r.iy, -r.py), ty1 = fmaf(N.b[8 + c], r.iy, -r.py);
+        const float tz0 = fmaf(N.b[4 + c], r.iz, -r.pz), tz1 = fmaf(N.b[10 + c], r.iz, -r.pz);
+        tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
+        return tn <= tf;
+    };
+    hl = one(0, tl);
+    hr = one(1, tr);
 }
 
 #ifdef RT_STATS
@@ -496,6 +504,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
     int32_t fbest = -1;                                       // FROZEN: fsph index of the best hit
     int sp = 0;
     int32_t node = FROZEN ? sc.fbvh2_root : sc.bvh2_root, pend = kDone;
+    float tcap = f32_up(closest);                              // box t range, updated after each leaf
 #ifdef RT_STATS
     uint32_t n_node = 0, n_leaf = 0, n_sph = 0, n_msph = 0, n_inner = 0, n_outer = 0;
 #endif
@@ -516,10 +525,9 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 ++n_node;
 #endif
                 const BvhNode2 N = nodes[node];
-                const float tcap = f32_up(closest);
                 float tl, tr;
-                const bool hl = box_hit_t(N.lbox, br, tcap, tl);
-                const bool hr = box_hit_t(N.rbox, br, tcap, tr);
+                bool hl, hr;
+                node_hit(N, br, tcap, hl, hr, tl, tr);
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
                     if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
@@ -566,6 +574,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 }
             }
             pend = kDone;
+            tcap = f32_up(closest);
         }
     }
     if (FROZEN && fbest >= 0) best = sc.fid[fbest];
@@ -614,8 +623,8 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                 const BvhNode2 N = sc.bvh2[node];
                 const float tcap = f32_up(closest * tscale);
                 float tl, tr;
-                const bool hl = box_hit_t(N.lbox, br, tcap, tl);
-                const bool hr = box_hit_t(N.rbox, br, tcap, tr);
+                bool hl, hr;
+                node_hit(N, br, tcap, hl, hr, tl, tr);
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
                     if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
@@ -1479,10 +1488,11 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
 template <int F>
-__global__ __launch_bounds__(256) void k_finish(const DevScene sc, const RenderParams rp, const PathState st,
+__global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
                                                 const bool depth0) {
+    const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
     // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in k_extend_lds
@@ -1601,7 +1611,7 @@ static uint32_t finish_blocks() {            // persistent tail grid (RTAMD_FINI
 static int scene_features(const DevScene& sc) {
     return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
 }
-hipError_t launch_extend(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
+hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
                          uint32_t* counts, bool depth0, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
@@ -1671,7 +1681,7 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
 #undef RT_SHADE
     return hipGetLastError();
 }
-hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
+hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, unsigned long long* seg_count, size_t tree0_budget, bool depth0,
                          hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
@@ -1682,7 +1692,7 @@ hipError_t launch_finish(const DevScene& sc, const RenderParams& rp, const PathS
     const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
     if (tree0_lds) lds += tree;
 #define RT_FINISH_F(F) \
-    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, seg_count, tree0_lds, depth0)
+    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth0)
     switch (scene_features(sc)) {
     case 0: RT_FINISH_F(0); break;
     case 1: RT_FINISH_F(1); break;
