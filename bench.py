@@ -28,18 +28,19 @@ sys.path.insert(0, os.path.join(ROOT, "scheme-raytrace_amd"))
 METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector spec (FMA = 2 flops)
-# Algorithmic HBM bytes of k_extend: every segment reads its
-# ray o,d,time (7 x f64 = 56 B); a hit writes t (8) + leaf id (4) + its queue
-# entry (4) = 16 B; a miss instead reads throughput (24) + work id (4) and
-# writes the sample colour (24) = 52 B.  Misses are counted as one per path
-# (each path ends in the sky except the few absorbed / depth-capped ones), so
-# the figure is an upper bound within ~1%.
-EXTEND_BYTES_PER_SEGMENT = 56 + 16
-EXTEND_BYTES_PER_MISS_EXTRA = 52 - 16
+# Algorithmic HBM bytes of the extend kernels: every segment
+# reads its ray record o, d (6 x f64 = 48 B); a hit writes t (8) + leaf id (4)
+# + its queue entry (4) = 16 B; a miss instead reads throughput + work id
+# (28 B) and writes the sample colour (24 B) = 52 B, i.e. 36 B more.  Per
+# path add the camera ray's time (8 B, depth-0 state) and one miss (each path
+# ends in the sky except the few absorbed / depth-capped ones: an upper bound
+# within ~1%).
+EXTEND_BYTES_PER_SEGMENT = 48 + 16
+EXTEND_BYTES_PER_PATH = 8 + (52 - 16)
 
 
 def extend_bytes(segments, paths):
-    return EXTEND_BYTES_PER_SEGMENT * segments + EXTEND_BYTES_PER_MISS_EXTRA * paths
+    return EXTEND_BYTES_PER_SEGMENT * segments + EXTEND_BYTES_PER_PATH * paths
 
 
 def parse():
@@ -228,6 +229,8 @@ def main():
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
             "ms_finish_per_step": round(ms_fin / a.steps, 3),
+            "extend_rays_per_step": round((segs - tail_segs) / a.steps), "paths_per_step": round(paths / a.steps),
+            "tail_segments_per_step": round(tail_segs / a.steps),
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, nx, ny, a.seed, a.cpu_baseline_seconds)

@@ -90,7 +90,7 @@ struct Context {
 // long, narrow tail of one chunk (its last few paths bouncing to depth 100)
 // overlaps the wide first iterations of the next one instead of leaving the
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
-constexpr int kLanes = 2;
+constexpr int kLanes = 4;                  // most lanes a render may use (RTAMD_LANES)
 struct Lane {
     DevBuf st_a, st_b, hit, sb, counts, queues, seg_tail;
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
@@ -889,7 +889,7 @@ size_t max_paths() {
 
 int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = no overlap)
     const char* e = std::getenv("RTAMD_LANES");
-    return e ? std::max(1, std::atoi(e)) : kLanes;
+    return e ? std::max(1, std::atoi(e)) : 2;
 }
 
 bool debug_counts() {

@@ -11,14 +11,14 @@ R=$PWD
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- \
-  python3 bench.py --spp 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/kt.log 2>&1
+  python3 bench.py --spp 256 --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_extend -f csv -d $O/fetch -o f -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events > $O/fetch.log 2>&1
+  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_extend -f csv -d $O/write -o w -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events > $O/write.log 2>&1
+  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU \
   --kernel-include-regex k_extend -f csv -d $O/sq -o s -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events > $O/sq.log 2>&1
-python3 tools/pmc_to_json.py $O/fetch/f_counter_collection.csv $O/write/w_counter_collection.csv cover \
+  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/sq.log 2>&1
+python3 tools/pmc_to_json.py $O/fetch/f_counter_collection.csv $O/write/w_counter_collection.csv $O/fetch.log cover \
   profiles/pmc_extend.json $O/sq/s_counter_collection.csv
 cp profiles/pmc_extend.json $O/
