@@ -31,8 +31,13 @@ hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, 
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
 hipError_t extend_lds_prepare(size_t, uint32_t*);
+size_t camera_lds_bytes(const DevScene&);
+hipError_t camera_prepare(const DevScene&, size_t, uint32_t*);
+hipError_t launch_camera(const DevScene&, const RenderParams&, const PathState&, uint32_t, const HitBuf&, uint32_t*,
+                         uint32_t, uint32_t, uint32_t*, size_t, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
-                             const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, hipStream_t);
+                             const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, unsigned long long*,
+                             hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 }  // namespace rtamd
 
@@ -103,6 +108,7 @@ struct Lane {
     // the chunk in flight
     enum State { IDLE, RUNNING, DONE } state = IDLE;
     int chunk = -1, depth = 0;
+    bool fused_camera = false;                 // depth 0 runs k_camera (no raygen pass)
     uint32_t n = 0, S = 0;
     uint64_t seq = 0;                          // enqueue order of the pending iteration
     RenderParams rp{};
@@ -137,6 +143,8 @@ struct Scene {
     DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
     uint32_t ext_lds_blocks = 0;
+    size_t cam_lds = 0;                            // k_camera (fused raygen + depth-0 extend), same
+    uint32_t cam_blocks = 0;
     // render buffers: one path pool per lane (render_impl)
     DevBuf pixlist;
     std::unique_ptr<Lane> lanes[kLanes];
@@ -558,6 +566,7 @@ int commit_scene(Scene* s, int world) {
     std::vector<SphereRec> fsph;
     std::vector<std::pair<int, int>> fsrc;           // (LEAF_SPHERE | LEAF_MSPHERE, local)
     int32_t fbvh2_root = 0;
+    bool tree0_any_time = false;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         // sphere trees: one primitive per leaf (measured fastest); curve trees keep 2
@@ -618,7 +627,10 @@ int commit_scene(Scene* s, int world) {
         // whose center is computed here with the kernel's own operations
         // (c0 + dc * ((0 - t0) / den), IEEE f64, no contraction), so the
         // primitive test it runs is bit-for-bit the moving-sphere test.
-        if (!bvh_has_bez && nm[refs.size()] > 0 && !std::getenv("RTAMD_NO_BVH0")) {
+        // (Built for every sphere tree: with no moving spheres it equals the
+        // all-times tree and serves every ray, tree0_any_time.)
+        tree0_any_time = nm[refs.size()] == 0;
+        if (!bvh_has_bez && !std::getenv("RTAMD_NO_BVH0")) {
             std::vector<PrimRef> refs0;
             for (size_t i = 0; i < refs.size(); ++i) {
                 PrimRef r = refs[i];
@@ -807,18 +819,9 @@ int commit_scene(Scene* s, int world) {
         if (int rc = upload(s->d_fid, fid, &d.fid)) return rc;
         d.fbvh2_root = fbvh2_root;
         d.n_fbvh2 = (int)fbvh2.size(); d.n_fbleaf = (int)fbleaf.size(); d.n_fsph = (int)fsph.size();
+        d.tree0_any_time = tree0_any_time ? 1 : 0;
     }
-    s->ext_lds = 0;
-    s->ext_lds_blocks = 0;
-    if (!std::getenv("RTAMD_NO_EXTEND_LDS")) {
-        const size_t lds = extend_lds_bytes(d);
-        uint32_t mb = 0;
-        if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(lds, &mb) == hipSuccess && mb >= 256) {
-            s->ext_lds = lds;
-            s->ext_lds_blocks = mb;
-        }
-        (void)hipGetLastError();
-    }
+    d.n_bleaf = (int)bleaf.size();
     d.lane_stack = lane_stack;
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
@@ -859,6 +862,30 @@ int commit_scene(Scene* s, int world) {
     d.cam.lens = cm[21]; d.cam.t0 = cm[22]; d.cam.t1 = cm[23];
     for (const Obj& o : s->objs)
         if (o.mat >= (int)s->mats.size()) return fail("object refers to an unknown material");
+    // LDS footprints of the persistent kernels: only now is every count and
+    // the stack depth in `d` final (the kernels carve their LDS from the same fields)
+    s->ext_lds = 0;
+    s->ext_lds_blocks = 0;
+    if (!std::getenv("RTAMD_NO_EXTEND_LDS")) {
+        const size_t lds = extend_lds_bytes(d);
+        uint32_t mb = 0;
+        if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(lds, &mb) == hipSuccess && mb >= 256) {
+            s->ext_lds = lds;
+            s->ext_lds_blocks = mb;
+        }
+        (void)hipGetLastError();
+    }
+    s->cam_lds = 0;
+    s->cam_blocks = 0;
+    if (!std::getenv("RTAMD_NO_CAMERA_LDS")) {
+        const size_t lds = camera_lds_bytes(d);
+        uint32_t mb = 0;
+        if (lds > 0 && lds <= extend_lds_budget() && camera_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
+            s->cam_lds = lds;
+            s->cam_blocks = mb;
+        }
+        (void)hipGetLastError();
+    }
     HIPCHK(s->d_dev.ensure(sizeof(DevScene)));
     HIPCHK(hipMemcpy(s->d_dev.p, &d, sizeof(DevScene), hipMemcpyHostToDevice));
     s->committed = true;
@@ -979,10 +1006,10 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         HIPCHK(L.sb.ensure(cap * 3 * sizeof(double)));
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(L.queues.ensure(scap * 4 * sizeof(uint32_t)));
-        HIPCHK(L.seg_tail.ensure(2 * sizeof(unsigned long long)));   // tail segments, next tail path
+        HIPCHK(L.seg_tail.ensure(3 * sizeof(unsigned long long)));   // tail segments, next tail path, errors
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
-        HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 2 * sizeof(unsigned long long), L.stream));
+        HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 3 * sizeof(unsigned long long), L.stream));
         L.A = carve_state(L.st_a.p, scap);
         L.B = carve_state(L.st_b.p, scap);
         L.state = Lane::IDLE;
@@ -1024,9 +1051,12 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         HitBuf hit{L.hit.as<HitRec>()};
         uint32_t* queues = L.queues.as<uint32_t>();
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[0], L.stream));
-        if (L.depth > 0 && s->ext_lds)          // every ray of a depth >= 1 launch has time +0.0
+        if (L.depth == 0 && L.fused_camera)     // raygen + first closest hit in one kernel
+            HIPCHK(launch_camera(s->dev, L.rp, *L.cur, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+                                 s->cam_lds, s->cam_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
+        else if (L.depth > 0 && s->ext_lds)     // every ray of a depth >= 1 launch has time +0.0
             HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap,
-                                     cnt, s->ext_lds_blocks, L.stream));
+                                     cnt, s->ext_lds_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
         else
             HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
                                  L.depth == 0, L.stream));
@@ -1084,7 +1114,9 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         rp.sb = L.sb.as<double>();
         rp.B = npix * L.S;
         HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
-        HIPCHK(launch_raygen(s->dev, rp, L.A, L.stream));
+        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / tail_divisor());
+        L.fused_camera = s->cam_lds != 0 && rp.B > tail;     // the tail kernel starts from raygen's state
+        if (!L.fused_camera) HIPCHK(launch_raygen(s->dev, rp, L.A, L.stream));
         L.cur = &L.A;
         L.nxt = &L.B;
         L.view = QView{nullptr, (uint32_t)scap};         // raygen output: contiguous
@@ -1138,9 +1170,11 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     for (int li = 0; li < nlanes; ++li) HIPCHK(hipStreamSynchronize(s->lanes[li]->stream));
     for (int li = 0; li < nlanes; ++li) {
         Lane& L = *s->lanes[li];
-        unsigned long long tail_segs = 0;
-        HIPCHK(hipMemcpy(&tail_segs, L.seg_tail.p, sizeof tail_segs, hipMemcpyDeviceToHost));
-        s->stats.segments += tail_segs;
+        unsigned long long ctl[3] = {0, 0, 0};
+        HIPCHK(hipMemcpy(ctl, L.seg_tail.p, sizeof ctl, hipMemcpyDeviceToHost));
+        if (ctl[2]) return fail("internal: a persistent kernel's LDS allocation was too small (flags " +
+                                std::to_string(ctl[2]) + ")");
+        s->stats.segments += ctl[0];
         for (size_t k = 0; k < L.n_fin; ++k) {
             float a = 0;
             HIPCHK(hipEventElapsedTime(&a, L.ev_fin[k].first, L.ev_fin[k].second));

@@ -41,7 +41,7 @@ struct DevMaterial {           // material.scm:24-111
 // Extend-side records: only what the closest-hit test reads, 16-B aligned so
 // the scalar unit fetches each with one s_load_dwordx8 / x16.
 struct alignas(32) SphereRec { double cx, cy, cz, rr; };             // rr = r*r
-struct alignas(64) MSphereRec {                                        // center(t) = c0 + dc*((t-t0)/den)
+struct alignas(32) MSphereRec {                                        // center(t) = c0 + dc*((t-t0)/den), 96 B
     double c0x, c0y, c0z, rr, dcx, dcy, dcz, t0;
     double den, pad0, pad1, pad2;
 };
@@ -124,6 +124,8 @@ struct DevScene {
     const BvhNode2* fbvh2; const BvhLeaf* fbleaf; int32_t fbvh2_root;
     const SphereRec* fsph; const int32_t* fid;
     int32_t n_fbvh2, n_fbleaf, n_fsph;
+    int32_t tree0_any_time;                        // no moving spheres in the tree: the time-0 tree serves every ray
+    int32_t n_bleaf;                               // leaves of the all-times tree
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
     int32_t leaf_base[kLeafTypes];             // first leaf id of each LeafType

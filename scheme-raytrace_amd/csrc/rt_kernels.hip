@@ -116,16 +116,15 @@ __device__ __forceinline__ void chain_hit(const Chain& c, v3& p, v3& n) {
 // =====================================================================
 // k_raygen — one camera sample per work item w = s_rel*npix + q
 // =====================================================================
-__global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderParams rp,
-                                                PathState st) {
-    const uint32_t w = blockIdx.x * 256u + threadIdx.x;
-    if (w >= rp.B) return;
+// trace-all's per-pixel jitter + cam:get-ray for work item w (main.scm:476-478,
+// camera.scm:80-92); returns the ray and leaves g after its draws.
+__device__ __forceinline__ void camera_ray(const DevScene& sc, const RenderParams& rp, const uint32_t w, v3& o, v3& d,
+                                           double& time, Rng& g) {
     const uint32_t s_rel = w / rp.npix;
     const uint32_t q = w - s_rel * rp.npix;
     const uint32_t j = rp.pixlist[q];
     const uint32_t y = j / rp.nx, x = j - y * rp.nx;
     const uint32_t smp = rp.spp0 + s_rel;
-    Rng g;
     g.init(rp.k0, rp.k1, j, smp, 0u);
     // main.scm:476-477 (let* order: u then v)
     const double u = ((double)x + g.next()) / (double)rp.nx;
@@ -141,11 +140,21 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
     const v3 rd = p * c.lens;
     const v3 cu = mk(c.u[0], c.u[1], c.u[2]), cv = mk(c.v[0], c.v[1], c.v[2]);
     const v3 offset = cu * rd.x + cv * rd.y;
-    const double time = c.t0 + g.next() * (c.t1 - c.t0);
+    time = c.t0 + g.next() * (c.t1 - c.t0);
     const v3 origin = mk(c.origin[0], c.origin[1], c.origin[2]);
-    const v3 o = origin + offset;
-    const v3 d = ((mk(c.llc[0], c.llc[1], c.llc[2]) + mk(c.hor[0], c.hor[1], c.hor[2]) * u) +
-                  mk(c.ver[0], c.ver[1], c.ver[2]) * v) - origin - offset;
+    o = origin + offset;
+    d = ((mk(c.llc[0], c.llc[1], c.llc[2]) + mk(c.hor[0], c.hor[1], c.hor[2]) * u) +
+         mk(c.ver[0], c.ver[1], c.ver[2]) * v) - origin - offset;
+}
+
+__global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderParams rp,
+                                                PathState st) {
+    const uint32_t w = blockIdx.x * 256u + threadIdx.x;
+    if (w >= rp.B) return;
+    v3 o, d;
+    double time;
+    Rng g;
+    camera_ray(sc, rp, w, o, d, time, g);
     st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};      // depth-0 state (rt_device.h PathState)
     st.tm[w] = time;
     st.rng0[w] = g.ctr;
@@ -490,12 +499,18 @@ __device__ unsigned long long g_stats[32];
 // FROZEN: the time-0 tree (DevScene::fbvh2), whose leaves hold plain sphere
 // records (moving spheres at center(0)); otherwise the all-times tree.
 // nodes / leaves / fsph may point into LDS (k_extend_lds) or HBM.
-template <bool FROZEN>
+__device__ __forceinline__ int32_t stack_ref(const uint32_t e) { return (int32_t)e; }
+__device__ __forceinline__ int32_t stack_ref(const uint16_t e) { return (int32_t)(int16_t)e; }   // sign: leaf refs < 0
+// SE: stack entry type — uint32_t, or uint16_t (k_extend_lds / k_camera, trees
+// under 32768 nodes and leaves: child refs fit int16, halving the LDS stack).
+template <bool FROZEN, class SE = uint32_t>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
-                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
+                                                 double& closest, int32_t& best, SE* lstk, const int lmax,
                                                  const BvhNode2* __restrict__ nodes,
                                                  const BvhLeaf* __restrict__ leaves,
-                                                 const SphereRec* __restrict__ fsph) {
+                                                 const SphereRec* __restrict__ fsph,
+                                                 const SphereRec* __restrict__ sph = nullptr,
+                                                 const MSphereRec* __restrict__ msph = nullptr) {
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d);
     const BoxRay br = box_ray(o, d);
@@ -519,7 +534,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             if (node < 0) {                                   // a leaf
                 if (pend != kDone) break;                     // one is already parked
                 pend = node;
-                node = sp ? (int32_t)lstk[--sp * stride] : kDone;
+                node = sp ? stack_ref(lstk[--sp * stride]) : kDone;
             } else {
 #ifdef RT_STATS
                 ++n_node;
@@ -530,14 +545,14 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 node_hit(N, br, tcap, hl, hr, tl, tr);
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
-                    if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                    if (sp < lmax) { lstk[sp * stride] = (SE)(lfirst ? N.r : N.l); ++sp; }
                     node = lfirst ? N.l : N.r;
                 } else if (hl) {
                     node = N.l;
                 } else if (hr) {
                     node = N.r;
                 } else {
-                    node = sp ? (int32_t)lstk[--sp * stride] : kDone;
+                    node = sp ? stack_ref(lstk[--sp * stride]) : kDone;
                 }
             }
             if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
@@ -560,14 +575,14 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 #ifdef RT_STATS
                     ++n_sph;
 #endif
-                    const SphereRec S = sc.sph[s];
+                    const SphereRec S = sph[s];
                     sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
                 }
                 for (int s = L.mb; s < L.mb + L.mn; ++s) {
 #ifdef RT_STATS
                     ++n_msph;
 #endif
-                    const MSphereRec S = sc.msph[s];
+                    const MSphereRec S = msph[s];
                     const double frac = (time - S.t0) / S.den;
                     const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                     sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
@@ -822,11 +837,15 @@ __device__ __forceinline__ bool medium_test(const DevScene& sc, const MediumRec&
 // The time-0 tree a kernel traverses (k_extend_lds stages it in LDS).
 struct Tree0 { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; };
 __device__ __forceinline__ Tree0 tree0_hbm(const DevScene& sc) { return Tree0{sc.fbvh2, sc.fbleaf, sc.fsph}; }
+// The all-times tree (k_camera stages it in LDS when the scene has moving spheres).
+struct TreeA { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; const MSphereRec* msph; };
+__device__ __forceinline__ TreeA treeA_hbm(const DevScene& sc) { return TreeA{sc.bvh2, sc.bleaf, sc.sph, sc.msph}; }
 
-template <int F>
+template <int F, class SE = uint32_t>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
-                                               const double time, double& closest, uint32_t* lstk,
-                                               const int lmax, BezWave* bw, Rng* rng, const Tree0 t0) {
+                                               const double time, double& closest, SE* lstk,
+                                               const int lmax, BezWave* bw, Rng* rng, const Tree0 t0,
+                                               const TreeA ta) {
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     int32_t best = -1;
@@ -834,10 +853,12 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
     for (int g = 0; g < sc.n_groups; ++g) {
         const Group G = sc.groups[g];
         if (G.type == GROUP_BVH) {
-            if (BEZ && sc.bvh_has_bez) bvh_closest_curves(sc, o0, d0, time, closest, best, lstk, lmax, *bw);
-            else if (sc.fbvh2 && __double_as_longlong(time) == 0ll)    // time +0.0: the time-0 tree
-                bvh_closest_lane<true>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph);
-            else bvh_closest_lane<false>(sc, o0, d0, time, closest, best, lstk, lmax, sc.bvh2, sc.bleaf, nullptr);
+            if (BEZ && sc.bvh_has_bez)
+                bvh_closest_curves(sc, o0, d0, time, closest, best, reinterpret_cast<uint32_t*>(lstk), lmax, *bw);
+            else if (sc.fbvh2 && (sc.tree0_any_time || __double_as_longlong(time) == 0ll))   // the time-0 tree
+                bvh_closest_lane<true, SE>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph);
+            else bvh_closest_lane<false, SE>(sc, o0, d0, time, closest, best, lstk, lmax, ta.nodes, ta.leaves, nullptr,
+                                         ta.sph, ta.msph);
             continue;
         }
         v3 o = o0, d = d0;
@@ -1042,7 +1063,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
             g.init(rp.k0, rp.k1, pix, smp, depth0 ? st.rng0[i] : st.path[i].rng);
         }
         const int32_t leaf = closest_hit<F>(sc, o, d, depth0 ? st.tm[i] : 0.0, t, s_lstack + threadIdx.x, LS,
-                                            &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc));
+                                            &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, tree0_hbm(sc), treeA_hbm(sc));
         if (MED) {                                   // draws taken inside media
             if (depth0) st.rng0[i] = g.ctr; else st.path[i].rng = g.ctr;
         }
@@ -1067,13 +1088,6 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
 }
 
-// =====================================================================
-// k_extend_lds — k_extend for launches whose rays all carry time +0.0 (every
-// depth >= 1 launch) in scenes whose time-0 tree fits in LDS: persistent
-// blocks stage the tree (nodes, leaves, sphere records) into LDS once and
-// grid-stride over the queue, so node fetches cost LDS latency instead of
-// L1/L2 latency.  Sphere scenes only (no curves, media or Klein: F = 0).
-// =====================================================================
 #ifndef RT_EXTLDS_BLOCK
 #define RT_EXTLDS_BLOCK 512
 #endif
@@ -1081,27 +1095,57 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
 #define RT_EXTLDS_WAVES 6
 #endif
 constexpr int kExtLdsBlock = RT_EXTLDS_BLOCK;
+// Copy n records of T from HBM into LDS, 16-B words, all threads of the block.
+template <class T>
+__device__ __forceinline__ void stage_lds(T* dst, const T* src, const int n, const int nthreads) {
+    static_assert(sizeof(T) % 16 == 0, "records are whole 16-B words");
+    const uint4* g = reinterpret_cast<const uint4*>(src);
+    uint4* l = reinterpret_cast<uint4*>(dst);
+    const int words = n * (int)(sizeof(T) / 16);
+    for (int k = threadIdx.x; k < words; k += nthreads) l[k] = g[k];
+}
+
+// Dynamic LDS the persistent kernels carve (host and device use the same
+// formula: the kernels check it against the allocation they were given).
+__host__ __device__ __forceinline__ size_t extend_lds_need(const DevScene& sc) {
+    return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+           (size_t)sc.n_fsph * sizeof(SphereRec) +
+           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t);
+}
+__host__ __device__ __forceinline__ size_t camera_lds_need(const DevScene& sc) {     // all-times tree
+    return (size_t)sc.n_bvh2 * sizeof(BvhNode2) + (size_t)sc.n_bleaf * sizeof(BvhLeaf) +
+           (size_t)sc.n_sph * sizeof(SphereRec) + (size_t)sc.n_msph * sizeof(MSphereRec) +
+           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t);
+}
+
+// =====================================================================
+// k_extend_lds — k_extend for launches whose rays all carry time +0.0 (every
+// depth >= 1 launch) in scenes whose time-0 tree fits in LDS: persistent
+// blocks stage the tree (nodes, leaves, sphere records) into LDS once and
+// grid-stride over the queue, so node fetches cost LDS latency instead of
+// L1/L2 latency.  Sphere scenes only (no curves, media or Klein: F = 0).
+// =====================================================================
+
 __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(const DevScene sc, const RenderParams rp,
                                                              const PathState st, const QView in, uint32_t n,
                                                              HitBuf hit, uint32_t* __restrict__ queues,
                                                              uint32_t qstride, uint32_t shard_cap,
-                                                             uint32_t* __restrict__ counts) {
+                                                             uint32_t* __restrict__ counts, const uint32_t lds_bytes,
+                                                             unsigned long long* __restrict__ err) {
     extern __shared__ uint4 s_dyn[];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
     const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
+    if (extend_lds_need(sc) > lds_bytes) {            // the carve below would leave the allocation
+        if (threadIdx.x == 0) atomicOr(err, 1ull);
+        return;
+    }
     BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_dyn);
     BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
     SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
-    uint32_t* s_lstack = reinterpret_cast<uint32_t*>(s_sph + ns);
-    {   // stage the time-0 tree (16-B words, coalesced)
-        const uint4* g; uint4* l;
-        g = reinterpret_cast<const uint4*>(sc.fbvh2); l = reinterpret_cast<uint4*>(s_nodes);
-        for (int k = threadIdx.x; k < nn * 4; k += kExtLdsBlock) l[k] = g[k];
-        g = reinterpret_cast<const uint4*>(sc.fbleaf); l = reinterpret_cast<uint4*>(s_leaves);
-        for (int k = threadIdx.x; k < nl * 2; k += kExtLdsBlock) l[k] = g[k];
-        g = reinterpret_cast<const uint4*>(sc.fsph); l = reinterpret_cast<uint4*>(s_sph);
-        for (int k = threadIdx.x; k < ns * 2; k += kExtLdsBlock) l[k] = g[k];
-    }
+    uint16_t* s_lstack = reinterpret_cast<uint16_t*>(s_sph + ns);
+    stage_lds(s_nodes, sc.fbvh2, nn, kExtLdsBlock);      // the time-0 tree
+    stage_lds(s_leaves, sc.fbleaf, nl, kExtLdsBlock);
+    stage_lds(s_sph, sc.fsph, ns, kExtLdsBlock);
     __syncthreads();
     const Tree0 t0{s_nodes, s_leaves, s_sph};
     const int LS = sc.lane_stack;
@@ -1116,7 +1160,8 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
             const v3 o = mk(R.ox, R.oy, R.oz);
             const v3 d = mk(R.dx, R.dy, R.dz);
             double t;
-            const int32_t leaf = closest_hit<0>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, nullptr, nullptr, t0);
+            const int32_t leaf = closest_hit<0, uint16_t>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, nullptr, nullptr, t0,
+                                                treeA_hbm(sc));
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);
                 const PathRec P = st.path[i];
@@ -1130,6 +1175,72 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
         if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+    }
+}
+
+// =====================================================================
+// k_camera — raygen and the first closest-hit query in one persistent kernel
+// (depth 0, sphere scenes): each work item's camera ray is traced where it is
+// made, against a tree staged in LDS once per block — the all-times tree
+// (ALL: the scene has moving spheres, camera rays carry shutter times) or the
+// time-0 tree (no moving spheres: it serves every time).  Only rays that hit
+// something store their depth-0 state for the shade kernels.
+// =====================================================================
+template <bool ALL>
+__global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const DevScene sc, const RenderParams rp,
+                                                                          const PathState st, const uint32_t n,
+                                                                          HitBuf hit, uint32_t* __restrict__ queues,
+                                                                          uint32_t qstride, uint32_t shard_cap,
+                                                                          uint32_t* __restrict__ counts,
+                                                                          const uint32_t lds_bytes,
+                                                                          unsigned long long* __restrict__ err) {
+    extern __shared__ uint4 s_dyn[];
+    __shared__ uint32_t s_cnt[4 * 16 + 4];
+    if ((ALL ? camera_lds_need(sc) : extend_lds_need(sc)) > lds_bytes) {
+        if (threadIdx.x == 0) atomicOr(err, 2ull);
+        return;
+    }
+    const int nn = ALL ? sc.n_bvh2 : sc.n_fbvh2, nl = ALL ? sc.n_bleaf : sc.n_fbleaf;
+    const int ns = ALL ? sc.n_sph : sc.n_fsph, nm = ALL ? sc.n_msph : 0;
+    BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_dyn);
+    BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
+    SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
+    MSphereRec* s_msph = reinterpret_cast<MSphereRec*>(s_sph + ns);
+    uint16_t* s_lstack = reinterpret_cast<uint16_t*>(s_msph + nm);
+    stage_lds(s_nodes, ALL ? sc.bvh2 : sc.fbvh2, nn, kExtLdsBlock);
+    stage_lds(s_leaves, ALL ? sc.bleaf : sc.fbleaf, nl, kExtLdsBlock);
+    stage_lds(s_sph, ALL ? sc.sph : sc.fsph, ns, kExtLdsBlock);
+    if (ALL) stage_lds(s_msph, sc.msph, nm, kExtLdsBlock);
+    __syncthreads();
+    const Tree0 t0 = ALL ? tree0_hbm(sc) : Tree0{s_nodes, s_leaves, s_sph};
+    const TreeA ta = ALL ? TreeA{s_nodes, s_leaves, s_sph, s_msph} : treeA_hbm(sc);
+    const int LS = sc.lane_stack;
+    for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
+        const uint32_t w = base + threadIdx.x;
+        int cls = -1;
+        if (w < n) {
+            v3 o, d;
+            double time, t;
+            Rng g;
+            camera_ray(sc, rp, w, o, d, time, g);
+            // ALL: a camera ray whose time is +0.0 (shutter t0 = t1 = 0) takes the time-0 tree from HBM
+            const int32_t leaf = closest_hit<0, uint16_t>(sc, o, d, time, t, s_lstack + threadIdx.x, LS, nullptr, nullptr,
+                                                t0, ta);
+            if (leaf < 0) {
+                const v3 L = sky_radiance(sc, d);            // throughput 1: (* 1 x) = x
+                rp.sb[w] = 1.0 * L.x;
+                rp.sb[rp.B + w] = 1.0 * L.y;
+                rp.sb[2u * rp.B + w] = 1.0 * L.z;
+            } else {
+                st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};   // depth-0 state for the shade kernels
+                st.tm[w] = time;
+                st.rng0[w] = g.ctr;
+                hit.h[w] = HitRec{t, leaf, 0};
+                cls = sc.mats[sc.leaves[leaf].mat].type;
+            }
+        }
+        const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
+        if (cls >= 0) queues[(size_t)cls * qstride + slot] = w;
     }
 }
 
@@ -1223,6 +1334,22 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
     return mk(0.0, 0.0, 0.0);
 }
 
+// (expt x 5) (material.scm:73) as libm's correctly rounded pow(x, 5.0): x^5
+// in double-double (error-free products via fma, relative error < 2^-100
+// before the one final rounding), so it rounds like a correctly rounded pow
+// except within 2^-100 of a rounding boundary; ~15 instructions instead of
+// OCML's log/exp-based pow (which is itself only faithful, <= 1 ulp).
+__device__ __forceinline__ double pow5(const double x) {
+    const double x2 = x * x, x2l = fma(x, x, -x2);
+    double h = x2 * x2;
+    double l = fma(x2, x2, -h) + 2.0 * (x2 * x2l);
+    const double s = h + l;                                  // renormalise x^4
+    l = l - (s - h);
+    h = s;
+    const double h5 = h * x;
+    const double l5 = fma(h, x, -h5) + l * x;
+    return h5 + l5;
+}
 __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - n * (2.0 * dot(v, n)); }  // material.scm:41-43
 
 // --------------------------------------------- light sampling (f2 extension)
@@ -1427,7 +1554,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
             refracted = (rdir - outward * dt) * ni - outward * sqrt(disc);
             const double r0a = (1.0 - ref_idx) / (1.0 + ref_idx);   // schlick :69-74
             const double r0 = r0a * r0a;
-            prob = r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
+            prob = r0 + (1.0 - r0) * pow5(1.0 - cosine);
         }
         p.d = (g.next() < prob) ? reflected : refracted;   // attenuation (1,1,1)
     }
@@ -1509,13 +1636,9 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
         BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_fdyn + words);
         BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
         SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
-        const uint4* g; uint4* l;
-        g = reinterpret_cast<const uint4*>(sc.fbvh2); l = reinterpret_cast<uint4*>(s_nodes);
-        for (int k = threadIdx.x; k < nn * 4; k += 256) l[k] = g[k];
-        g = reinterpret_cast<const uint4*>(sc.fbleaf); l = reinterpret_cast<uint4*>(s_leaves);
-        for (int k = threadIdx.x; k < nl * 2; k += 256) l[k] = g[k];
-        g = reinterpret_cast<const uint4*>(sc.fsph); l = reinterpret_cast<uint4*>(s_sph);
-        for (int k = threadIdx.x; k < ns * 2; k += 256) l[k] = g[k];
+        stage_lds(s_nodes, sc.fbvh2, nn, 256);
+        stage_lds(s_leaves, sc.fbleaf, nl, 256);
+        stage_lds(s_sph, sc.fsph, ns, 256);
         t0 = Tree0{s_nodes, s_leaves, s_sph};
         __syncthreads();
     }
@@ -1551,7 +1674,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             Rng g;
             if (MED) g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
             const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
-                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, t0);
+                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, t0, treeA_hbm(sc));
             if (MED) p.rng = g.ctr;
             v3 L;
             bool cont = false;
@@ -1631,19 +1754,19 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
 // bytes of LDS k_extend_lds needs for the scene's time-0 tree (0 = cannot run)
 size_t extend_lds_bytes(const DevScene& sc) {
     if (!sc.fbvh2 || sc.n_bez || sc.n_med || sc.n_klein) return 0;
-    return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
-           (size_t)sc.n_fsph * sizeof(SphereRec) +
-           (size_t)kExtLdsBlock * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+    if (sc.n_fbvh2 >= 32768 || sc.n_fbleaf >= 32768) return 0;        // 16-bit stack entries
+    return extend_lds_need(sc);
 }
 hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                              uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride,
-                             uint32_t shard_cap, uint32_t* counts, uint32_t max_blocks, hipStream_t s) {
+                             uint32_t shard_cap, uint32_t* counts, uint32_t max_blocks, unsigned long long* err,
+                             hipStream_t s) {
     const size_t lds = extend_lds_bytes(sc);
     uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     blocks = (blocks + kShards - 1) / kShards * kShards;      // every shard gets the same number of blocks
     hipLaunchKernelGGL(k_extend_lds, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit, queues,
-                       qstride, shard_cap, counts);
+                       qstride, shard_cap, counts, (uint32_t)lds, err);
     return hipGetLastError();
 }
 // grid of k_extend_lds: every block it can keep resident on the device at once
@@ -1656,6 +1779,42 @@ hipError_t extend_lds_prepare(size_t lds, uint32_t* max_blocks) {
     HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_lds, kExtLdsBlock, lds));
     *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
     return hipSuccess;
+}
+// LDS bytes k_camera needs (0 = cannot run): the all-times tree when the scene
+// has moving spheres, else the time-0 tree
+size_t camera_lds_bytes(const DevScene& sc) {
+    if (!sc.fbvh2 || sc.n_bez || sc.n_med || sc.n_klein) return 0;
+    if (sc.tree0_any_time) return extend_lds_bytes(sc);
+    if (sc.n_bvh2 >= 32768 || sc.n_bleaf >= 32768) return 0;          // 16-bit stack entries
+    return camera_lds_need(sc);
+}
+hipError_t camera_prepare(const DevScene& sc, size_t lds, uint32_t* max_blocks) {
+    const void* f = sc.tree0_any_time ? reinterpret_cast<const void*>(&k_camera<false>)
+                                      : reinterpret_cast<const void*>(&k_camera<true>);
+    HIP_RETURN_IF(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_RETURN_IF(hipGetDevice(&dev));
+    HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (sc.tree0_any_time)
+        HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_camera<false>, kExtLdsBlock, lds));
+    else
+        HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_camera<true>, kExtLdsBlock, lds));
+    *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
+    return hipSuccess;
+}
+hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathState& st, uint32_t n,
+                         const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap, uint32_t* counts,
+                         size_t lds, uint32_t max_blocks, unsigned long long* err, hipStream_t s) {
+    uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
+    if (blocks > max_blocks) blocks = max_blocks;
+    blocks = (blocks + kShards - 1) / kShards * kShards;
+    if (sc.tree0_any_time)
+        hipLaunchKernelGGL(k_camera<false>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,
+                           qstride, shard_cap, counts, (uint32_t)lds, err);
+    else
+        hipLaunchKernelGGL(k_camera<true>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,
+                           qstride, shard_cap, counts, (uint32_t)lds, err);
+    return hipGetLastError();
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
