@@ -593,20 +593,19 @@ int commit_scene(Scene* s, int world) {
         flatten_bvh2(bvh_nodes, margin, [&](int b, int e) {
             return BvhLeaf{ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0};
         }, bvh2, bleaf, bvh2_root, lane_stack);
-        const int gid = (int)groups.size();
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
             const LeafTmp& L = f.leaves[r.leaf];
             const Obj& o = s->objs[L.obj];
             LeafInfo li{};
-            li.type = L.type; li.group = gid; li.mat = o.mat; li.flip = L.flip;
+            li.type = L.type; li.chain = -1; li.mat = o.mat; li.flip = L.flip;
             if (r.type == LEAF_SPHERE) {
-                li.inv_r = 1.0 / o.r; li.radius = o.r;
+                li.inv_r = 1.0 / o.r; 
                 li.local = (int)sph.size();
                 sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
                 lsph.push_back(li);
             } else if (r.type == LEAF_MSPHERE) {
-                li.inv_r = 1.0 / o.r; li.radius = o.r;
+                li.inv_r = 1.0 / o.r; 
                 li.local = (int)msph.size();
                 MSphereRec m{};
                 m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
@@ -680,17 +679,17 @@ int commit_scene(Scene* s, int world) {
     auto add_record = [&](const LeafTmp& L, LeafInfo* li_world) {
         const Obj& o = s->objs[L.obj];
         LeafInfo placeholder{};
-        placeholder.type = L.type; placeholder.group = -1; placeholder.mat = 0;
+        placeholder.type = L.type; placeholder.chain = -1; placeholder.mat = 0;
         LeafInfo* li = li_world ? li_world : &placeholder;
         if (L.type == LEAF_SPHERE) {
-            li->local = (int)sph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lsph.push_back(*li);
+            li->local = (int)sph.size(); li->inv_r = 1.0 / o.r;  lsph.push_back(*li);
             sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
         } else if (L.type == LEAF_MSPHERE) {
             MSphereRec m{};
             m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
             m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
             m.t0 = o.t0; m.den = o.t1 - o.t0;
-            li->local = (int)msph.size(); li->inv_r = 1.0 / o.r; li->radius = o.r; lmsph.push_back(*li);
+            li->local = (int)msph.size(); li->inv_r = 1.0 / o.r;  lmsph.push_back(*li);
             msph.push_back(m);
         } else if (L.type == LEAF_BEZIER) {
             li->local = (int)bez.size(); lbez.push_back(*li);
@@ -722,7 +721,7 @@ int commit_scene(Scene* s, int world) {
                     if (L->chain != ch || L->type != type) continue;
                     if (world) {
                         LeafInfo li{};
-                        li.type = type; li.group = (int)out.size(); li.mat = s->objs[L->obj].mat; li.flip = L->flip;
+                        li.type = type; li.chain = ch; li.mat = s->objs[L->obj].mat; li.flip = L->flip;
                         add_record(*L, &li);
                     } else {
                         add_record(*L, nullptr);
@@ -753,7 +752,7 @@ int commit_scene(Scene* s, int world) {
         m.bg_end = (int)bgroups.size();
         m.neg_inv_density = -(1 / o.r);             // (- (/ 1 density)), geometry.scm:564
         LeafInfo li{};
-        li.type = LEAF_MEDIUM; li.group = (int)groups.size(); li.local = (int)med.size();
+        li.type = LEAF_MEDIUM; li.chain = medium->chain; li.local = (int)med.size();
         li.mat = o.mat; li.flip = medium->flip;
         groups.push_back(Group{LEAF_MEDIUM, medium->chain, (int)med.size(), (int)med.size() + 1});
         med.push_back(m);
@@ -782,6 +781,36 @@ int commit_scene(Scene* s, int world) {
     for (auto& li : lmed) leaves.push_back(li);
     base[LEAF_KLEIN] = (int32_t)leaves.size();
     for (auto& li : lklein) leaves.push_back(li);
+    // the shade-side fields: material, texture shortcut, sphere centre (LeafInfo)
+    for (LeafInfo& li : leaves) {
+        if (li.mat < 0 || li.mat >= (int)s->mats.size()) continue;     // boundary placeholders
+        const DevMaterial& m = s->mats[li.mat];
+        li.mtype = m.type;
+        li.tex = m.tex;
+        li.mparam = (m.type == MAT_METAL) ? m.fuzz : m.ref_idx;
+        li.tex_kind = TK_GENERIC;
+        auto constant = [&](int t) { return t >= 0 && t < (int)s->texs.size() && s->texs[t].type == TEX_CONSTANT; };
+        if (constant(m.tex)) {
+            const DevTexture& T = s->texs[m.tex];
+            li.tex_kind = TK_CONSTANT;
+            li.albedo[0] = T.r; li.albedo[1] = T.g; li.albedo[2] = T.bl;
+        } else if (m.tex >= 0 && m.tex < (int)s->texs.size() && s->texs[m.tex].type == TEX_CHECKER &&
+                   constant(s->texs[m.tex].a) && constant(s->texs[m.tex].b)) {
+            const DevTexture& E = s->texs[s->texs[m.tex].a];       // even (texture.scm:20-23)
+            const DevTexture& O = s->texs[s->texs[m.tex].b];       // odd
+            li.tex_kind = TK_CHECKER_CONST;
+            li.albedo[0] = E.r; li.albedo[1] = E.g; li.albedo[2] = E.bl;
+            li.albedo2[0] = O.r; li.albedo2[1] = O.g; li.albedo2[2] = O.bl;
+        }
+        if (li.type == LEAF_SPHERE) {
+            const SphereRec& S = sph[(size_t)li.local];
+            li.c[0] = S.cx; li.c[1] = S.cy; li.c[2] = S.cz;
+        } else if (li.type == LEAF_MSPHERE) {                   // center(0), the kernel's own operations
+            const MSphereRec& M = msph[(size_t)li.local];
+            const double frac = (0.0 - M.t0) / M.den;
+            li.c[0] = M.c0x + M.dcx * frac; li.c[1] = M.c0y + M.dcy * frac; li.c[2] = M.c0z + M.dcz * frac;
+        }
+    }
 
     std::vector<Chain> chains;
     for (auto& cv : f.chains) {

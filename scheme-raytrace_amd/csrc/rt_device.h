@@ -74,12 +74,19 @@ struct alignas(64) BvhNode2 { float b[12]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
 constexpr int kLaneStack = 32;                 // max per-lane traversal stack (dynamic LDS, stride = block size)
 
-// Shade-side per-leaf record (indexed by leaf id).
-struct LeafInfo {
-    int32_t type, group, local, mat;   // local = index in the type's array
-    int32_t flip, pad0, pad1, pad2;
-    double inv_r;                      // sphere: (/ 1 radius) as a double
-    double radius;
+// Shade-side per-leaf record (indexed by leaf id): what a shade kernel reads
+// for a hit, in one 128-B record, so a hit costs one dependent load instead
+// of the chain leaf -> group -> primitive -> material -> texture.
+enum TexKind : int32_t { TK_GENERIC = 0, TK_CONSTANT = 1, TK_CHECKER_CONST = 2 };
+struct alignas(16) LeafInfo {
+    int32_t type, chain, local, flip;  // local = index in the type's array; chain: instance chain (-1 world)
+    int32_t mat, mtype, tex, tex_kind; // material id and type, its texture id and TexKind
+    double mparam;                     // fuzz (metal) / ref_idx (dielectric)
+    double inv_r;                      // sphere / moving sphere: (/ 1 radius) as a double
+    double c[3];                       // sphere center; moving sphere: center(0), for time-0 rays
+    double albedo[3];                  // TK_CONSTANT colour / TK_CHECKER_CONST even colour
+    double albedo2[3];                 // TK_CHECKER_CONST odd colour
+    double pad;
 };
 
 struct ChainOpRec { int32_t op, pad; double x, y, z; };   // translate: (x,y,z); rotate: x=sin, y=cos

@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
             }
         } else {
             hit.h[i] = HitRec{t, leaf, 0};
-            cls = sc.mats[sc.leaves[leaf].mat].type;
+            cls = sc.leaves[leaf].mtype;
         }
     }
     const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
                 rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
             } else {
                 hit.h[i] = HitRec{t, leaf, 0};
-                cls = sc.mats[sc.leaves[leaf].mat].type;
+                cls = sc.leaves[leaf].mtype;
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const 
                 st.tm[w] = time;
                 st.rng0[w] = g.ctr;
                 hit.h[w] = HitRec{t, leaf, 0};
-                cls = sc.mats[sc.leaves[leaf].mat].type;
+                cls = sc.leaves[leaf].mtype;
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
@@ -1350,6 +1350,15 @@ __device__ __forceinline__ double pow5(const double x) {
     const double l5 = fma(h, x, -h5) + l * x;
     return h5 + l5;
 }
+// a hit's texture value from its leaf record: constant and checker-of-constants
+// colours are inline (texture.scm:12-23); anything else goes through tex_value
+template <bool PN>
+__device__ __forceinline__ v3 leaf_tex(const DevScene& sc, const PerlinLds& P, const LeafInfo& li, const v3 p) {
+    if (li.tex_kind == TK_CONSTANT) return mk(li.albedo[0], li.albedo[1], li.albedo[2]);
+    if (li.tex_kind == TK_CHECKER_CONST)
+        return checker_odd(p) ? mk(li.albedo2[0], li.albedo2[1], li.albedo2[2]) : mk(li.albedo[0], li.albedo[1], li.albedo[2]);
+    return tex_value<PN>(sc, P, li.tex, p);
+}
 __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - n * (2.0 * dot(v, n)); }  // material.scm:41-43
 
 // --------------------------------------------- light sampling (f2 extension)
@@ -1424,18 +1433,21 @@ template <int MATF, bool PN = true, bool LS = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
                                           PathRegs& p, const double t, const int32_t leaf, v3& L) {
     L = mk(0.0, 0.0, 0.0);
-    const LeafInfo li = sc.leaves[leaf];
-    const Group G = sc.groups[li.group];
+    const LeafInfo& li = sc.leaves[leaf];                    // one record: geometry, material, texture (fields read where used)
     v3 o = p.o, d = p.d;
-    if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
+    if (li.chain >= 0) chain_ray(sc.chains[li.chain], o, d);
     v3 pt = o + d * t;                         // point-at-parameter on the (local) ray
     v3 nrm;
     if (li.type == LEAF_SPHERE) {
-        const SphereRec S = sc.sph[li.local];
-        nrm = (pt - mk(S.cx, S.cy, S.cz)) * li.inv_r;
+        nrm = (pt - mk(li.c[0], li.c[1], li.c[2])) * li.inv_r;
     } else if (li.type == LEAF_MSPHERE) {
-        const MSphereRec S = sc.msph[li.local];
-        const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * ((p.time - S.t0) / S.den);
+        v3 cen;
+        if (__double_as_longlong(p.time) == 0ll) {          // center(0), computed as below on the host
+            cen = mk(li.c[0], li.c[1], li.c[2]);
+        } else {
+            const MSphereRec S = sc.msph[li.local];
+            cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * ((p.time - S.t0) / S.den);
+        }
         nrm = (pt - cen) * li.inv_r;
     } else if (li.type == LEAF_RECT_XY) {
         nrm = mk(0.0, 0.0, 1.0);
@@ -1450,13 +1462,12 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         nrm = d * -1.0;                                      // curve: (v:scale (dir r) -1), bezier.scm:204
     }
     if (li.flip) nrm = nrm * -1.0;                          // flip-normals :438
-    if (G.chain >= 0) chain_hit(sc.chains[G.chain], pt, nrm);
-    const DevMaterial m = sc.mats[li.mat];
-    const int mt = (MATF >= 0) ? MATF : m.type;
+    if (li.chain >= 0) chain_hit(sc.chains[li.chain], pt, nrm);
+    const int mt = (MATF >= 0) ? MATF : li.mtype;
     const v3 rdir = p.d;
     const bool can_continue = p.depth < (uint32_t)kMaxDepth;
     if (mt == MAT_DIFFUSE_LIGHT) {                           // material.scm:103-111
-        if (dot(nrm, rdir) < 0.0) L = tex_value<PN>(sc, P, m.tex, pt);
+        if (dot(nrm, rdir) < 0.0) L = leaf_tex<PN>(sc, P, li, pt);
         return false;
     }
     if (!can_continue) return false;                         // depth cap (main.scm:112,119)
@@ -1491,7 +1502,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         if (cosine < 0.0) cosine = 0.0;
         const double spdf = cosine / kPi;
         const double ipdf = 1.0 / pdf_val;
-        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
+        const v3 att = leaf_tex<PN>(sc, P, li, pt);
         p.T = mk((p.T.x * (att.x * spdf)) * ipdf, (p.T.y * (att.y * spdf)) * ipdf,
                  (p.T.z * (att.z * spdf)) * ipdf);
         p.d = dir;
@@ -1519,7 +1530,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         if (cosine < 0.0) cosine = 0.0;
         const double spdf = cosine / kPi;                    // scattering-pdf
         const double ipdf = 1.0 / pdf;
-        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
+        const v3 att = leaf_tex<PN>(sc, P, li, pt);
         // forward form of  e + ((att*spdf) (*) L_next) * (1/pdf)  (main.scm:113-118)
         p.T = mk((p.T.x * (att.x * spdf)) * ipdf, (p.T.y * (att.y * spdf)) * ipdf,
                  (p.T.z * (att.z * spdf)) * ipdf);
@@ -1532,13 +1543,13 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
             s = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, c * 2.0 - 1.0);
             if (dot(s, s) < 1.0) break;
         }
-        const v3 sd = reflected + s * m.fuzz;
+        const v3 sd = reflected + s * li.mparam;
         if (!(dot(sd, nrm) > 0.0)) return false;             // absorbed: emitted 0
-        const v3 att = tex_value<PN>(sc, P, m.tex, pt);
+        const v3 att = leaf_tex<PN>(sc, P, li, pt);
         p.T = p.T * att;
         p.d = sd;
     } else {                                                 // dielectric material.scm:76-101 (R2)
-        const double ref_idx = m.ref_idx;
+        const double ref_idx = li.mparam;
         const v3 reflected = reflect(rdir, nrm);
         const double dd = dot(rdir, nrm);
         const v3 outward = (dd > 0.0) ? nrm * -1.0 : nrm;
