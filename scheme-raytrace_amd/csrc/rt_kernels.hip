@@ -1429,11 +1429,13 @@ __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g
 // otherwise L is the terminal radiance (emission or 0).
 // LS = false compiles the light-sampling mixture (f2) out: scenes without a
 // light target never take it, and its constants cost scalar registers.
+// leaves: the leaf records (LDS in k_shade when the table is small, else HBM)
 template <int MATF, bool PN = true, bool LS = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
-                                          PathRegs& p, const double t, const int32_t leaf, v3& L) {
+                                          PathRegs& p, const double t, const int32_t leaf, v3& L,
+                                          const LeafInfo* __restrict__ leaves) {
     L = mk(0.0, 0.0, 0.0);
-    const LeafInfo& li = sc.leaves[leaf];                    // one record: geometry, material, texture (fields read where used)
+    const LeafInfo& li = leaves[leaf];                       // one record: geometry, material, texture (fields read where used)
     v3 o = p.o, d = p.d;
     if (li.chain >= 0) chain_ray(sc.chains[li.chain], o, d);
     v3 pt = o + d * t;                         // point-at-parameter on the (local) ray
@@ -1587,7 +1589,7 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 // =====================================================================
 // k_shade<MAT> — one material's queue; survivors compacted into `out`
 // =====================================================================
-template <int MAT, bool PN, bool LS>
+template <int MAT, bool PN, bool LS, bool LL>
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 1
 #endif
@@ -1598,7 +1600,12 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
-    stage_perlin<PN>(sc, P);
+    extern __shared__ uint4 s_leafdyn[];             // LL: the leaf records, staged once per block
+    LeafInfo* s_leaves = reinterpret_cast<LeafInfo*>(s_leafdyn);
+    if (LL) stage_lds(s_leaves, sc.leaves, sc.n_leaves, 256);
+    stage_perlin<PN>(sc, P);                         // (its barrier also covers the leaf staging)
+    if (LL && !(PN && sc.has_perlin)) __syncthreads();
+    const LeafInfo* leaves = LL ? s_leaves : sc.leaves;
     const QMap qm = qmap(qv);
     uint32_t n = 0;
 #pragma unroll
@@ -1612,7 +1619,7 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
             load_path(in, i, p, rp, depth0);
             v3 L;
             const HitRec H = hit.h[i];
-            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L);
+            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
@@ -1690,7 +1697,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             v3 L;
             bool cont = false;
             if (leaf < 0) L = sky_radiance(sc, p.d);
-            else cont = shade_hit<-1>(sc, P, rp, p, t, leaf, L);
+            else cont = shade_hit<-1>(sc, P, rp, p, t, leaf, L, sc.leaves);
             if (!cont) { write_sample(rp, p, L); active = false; }
         }
     }
@@ -1827,6 +1834,11 @@ hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathS
                            qstride, shard_cap, counts, (uint32_t)lds, err);
     return hipGetLastError();
 }
+constexpr size_t kShadeLeafLds = 32768;      // stage the leaf records when they fit (256 leaves)
+static bool shade_leaves_hbm() {             // RTAMD_SHADE_LEAVES_HBM: keep them in HBM (A/B)
+    static const bool v = std::getenv("RTAMD_SHADE_LEAVES_HBM") != nullptr;
+    return v;
+}
 hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
                         const PathState& out, uint32_t* out_counts, uint32_t shard_cap, bool depth0, hipStream_t s) {
@@ -1834,11 +1846,19 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > 4096u) blocks = 4096u;
     if (blocks == 0u) blocks = kShards;
-#define RT_SHADE(M, PN, LS) \
-    hipLaunchKernelGGL((k_shade<M, PN, LS>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hit, queue, qv, out, \
-                       out_counts, shard_cap, depth0)
+#define RT_SHADE(M, PN, LS)                                                                                  \
+    do {                                                                                                     \
+        if (ll)                                                                                              \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hit,  \
+                               queue, qv, out, out_counts, shard_cap, depth0);                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hit,   \
+                               queue, qv, out, out_counts, shard_cap, depth0);                               \
+    } while (0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
+    const size_t lds = (size_t)sc.n_leaves * sizeof(LeafInfo);
+    const bool ll = lds <= kShadeLeafLds && !shade_leaves_hbm();
     switch (mat) {
     case MAT_LAMBERTIAN:
         if (ls) { if (pn) RT_SHADE(MAT_LAMBERTIAN, true, true); else RT_SHADE(MAT_LAMBERTIAN, false, true); }
