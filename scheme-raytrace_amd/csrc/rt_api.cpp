@@ -141,6 +141,7 @@ struct Scene {
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
     DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
+    DevBuf d_leaf_cls;
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
     uint32_t ext_lds_blocks = 0;
     size_t cam_lds = 0;                            // k_camera (fused raygen + depth-0 extend), same
@@ -855,6 +856,11 @@ int commit_scene(Scene* s, int world) {
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
     if (int rc = upload(s->d_leaves, leaves, &d.leaves)) return rc;
+    {
+        std::vector<uint8_t> lc((leaves.size() + 15) / 16 * 16 + 16, 0);
+        for (size_t k = 0; k < leaves.size(); ++k) lc[k] = (uint8_t)leaves[k].mtype;
+        if (int rc = upload(s->d_leaf_cls, lc, &d.leaf_cls)) return rc;
+    }
     if (int rc = upload(s->d_mats, s->mats, &d.mats)) return rc;
     if (int rc = upload(s->d_texs, s->texs, &d.texs)) return rc;
     d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();

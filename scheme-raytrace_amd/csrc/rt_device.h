@@ -135,6 +135,7 @@ struct DevScene {
     int32_t n_bleaf;                               // leaves of the all-times tree
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
+    const uint8_t* leaf_cls;                   // leaf id -> material type (a byte per leaf, padded to 16)
     int32_t leaf_base[kLeafTypes];             // first leaf id of each LeafType
     const DevMaterial* mats; int32_t n_mats;
     const DevTexture* texs;  int32_t n_texs;

@@ -510,7 +510,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                                                  const BvhLeaf* __restrict__ leaves,
                                                  const SphereRec* __restrict__ fsph,
                                                  const SphereRec* __restrict__ sph = nullptr,
-                                                 const MSphereRec* __restrict__ msph = nullptr) {
+                                                 const MSphereRec* __restrict__ msph = nullptr,
+                                                 const int32_t* __restrict__ fid = nullptr) {
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d);
     const BoxRay br = box_ray(o, d);
@@ -592,7 +593,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             tcap = f32_up(closest);
         }
     }
-    if (FROZEN && fbest >= 0) best = sc.fid[fbest];
+    if (FROZEN && fbest >= 0) best = fid[fbest];
 #ifdef RT_STATS
     constexpr int so = FROZEN ? 16 : 0;
     RT_STAT(so + 0, 1); RT_STAT(so + 1, n_node); RT_STAT(so + 2, n_leaf); RT_STAT(so + 3, n_sph);
@@ -835,8 +836,8 @@ __device__ __forceinline__ bool medium_test(const DevScene& sc, const MediumRec&
 }
 
 // The time-0 tree a kernel traverses (k_extend_lds stages it in LDS).
-struct Tree0 { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; };
-__device__ __forceinline__ Tree0 tree0_hbm(const DevScene& sc) { return Tree0{sc.fbvh2, sc.fbleaf, sc.fsph}; }
+struct Tree0 { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; const int32_t* fid; };
+__device__ __forceinline__ Tree0 tree0_hbm(const DevScene& sc) { return Tree0{sc.fbvh2, sc.fbleaf, sc.fsph, sc.fid}; }
 // The all-times tree (k_camera stages it in LDS when the scene has moving spheres).
 struct TreeA { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; const MSphereRec* msph; };
 __device__ __forceinline__ TreeA treeA_hbm(const DevScene& sc) { return TreeA{sc.bvh2, sc.bleaf, sc.sph, sc.msph}; }
@@ -856,7 +857,8 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
             if (BEZ && sc.bvh_has_bez)
                 bvh_closest_curves(sc, o0, d0, time, closest, best, reinterpret_cast<uint32_t*>(lstk), lmax, *bw);
             else if (sc.fbvh2 && (sc.tree0_any_time || __double_as_longlong(time) == 0ll))   // the time-0 tree
-                bvh_closest_lane<true, SE>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph);
+                bvh_closest_lane<true, SE>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph,
+                                           nullptr, nullptr, t0.fid);
             else bvh_closest_lane<false, SE>(sc, o0, d0, time, closest, best, lstk, lmax, ta.nodes, ta.leaves, nullptr,
                                          ta.sph, ta.msph);
             continue;
@@ -1107,15 +1109,26 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* src, const int n, con
 
 // Dynamic LDS the persistent kernels carve (host and device use the same
 // formula: the kernels check it against the allocation they were given).
+// Layout: tree nodes | leaves | sphere records [| moving spheres] | 16-bit
+// lane stacks | fsph -> leaf id (time-0 tree) | leaf -> material class (bytes).
+__host__ __device__ __forceinline__ size_t lds_tail_bytes(const DevScene& sc) {
+    return ((size_t)sc.n_fsph * 4 + 15) / 16 * 16 + ((size_t)sc.n_leaves + 15) / 16 * 16;
+}
 __host__ __device__ __forceinline__ size_t extend_lds_need(const DevScene& sc) {
     return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
            (size_t)sc.n_fsph * sizeof(SphereRec) +
-           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t);
+           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t) +
+           lds_tail_bytes(sc);
 }
 __host__ __device__ __forceinline__ size_t camera_lds_need(const DevScene& sc) {     // all-times tree
     return (size_t)sc.n_bvh2 * sizeof(BvhNode2) + (size_t)sc.n_bleaf * sizeof(BvhLeaf) +
            (size_t)sc.n_sph * sizeof(SphereRec) + (size_t)sc.n_msph * sizeof(MSphereRec) +
-           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t);
+           (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t) +
+           lds_tail_bytes(sc);
+}
+// stage n 32-bit words (fid, packed class bytes)
+__device__ __forceinline__ void stage_words(uint32_t* dst, const uint32_t* src, const int n, const int nthreads) {
+    for (int k = threadIdx.x; k < n; k += nthreads) dst[k] = src[k];
 }
 
 // =====================================================================
@@ -1143,11 +1156,16 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
     BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
     SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
     uint16_t* s_lstack = reinterpret_cast<uint16_t*>(s_sph + ns);
+    int32_t* s_fid = reinterpret_cast<int32_t*>(s_lstack + (size_t)kExtLdsBlock * (sc.lane_stack > 0 ? sc.lane_stack : 1));
+    uint8_t* s_cls = reinterpret_cast<uint8_t*>(s_fid) + ((size_t)ns * 4 + 15) / 16 * 16;
     stage_lds(s_nodes, sc.fbvh2, nn, kExtLdsBlock);      // the time-0 tree
     stage_lds(s_leaves, sc.fbleaf, nl, kExtLdsBlock);
     stage_lds(s_sph, sc.fsph, ns, kExtLdsBlock);
+    stage_words(reinterpret_cast<uint32_t*>(s_fid), reinterpret_cast<const uint32_t*>(sc.fid), ns, kExtLdsBlock);
+    stage_words(reinterpret_cast<uint32_t*>(s_cls), reinterpret_cast<const uint32_t*>(sc.leaf_cls),
+                (sc.n_leaves + 3) / 4, kExtLdsBlock);
     __syncthreads();
-    const Tree0 t0{s_nodes, s_leaves, s_sph};
+    const Tree0 t0{s_nodes, s_leaves, s_sph, s_fid};
     const int LS = sc.lane_stack;
     const QMap qm = qmap(in);
     for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
@@ -1170,7 +1188,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
                 rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
             } else {
                 hit.h[i] = HitRec{t, leaf, 0};
-                cls = sc.leaves[leaf].mtype;
+                cls = s_cls[leaf];
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
@@ -1207,12 +1225,17 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const 
     SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
     MSphereRec* s_msph = reinterpret_cast<MSphereRec*>(s_sph + ns);
     uint16_t* s_lstack = reinterpret_cast<uint16_t*>(s_msph + nm);
+    int32_t* s_fid = reinterpret_cast<int32_t*>(s_lstack + (size_t)kExtLdsBlock * (sc.lane_stack > 0 ? sc.lane_stack : 1));
+    uint8_t* s_cls = reinterpret_cast<uint8_t*>(s_fid) + ((size_t)sc.n_fsph * 4 + 15) / 16 * 16;
     stage_lds(s_nodes, ALL ? sc.bvh2 : sc.fbvh2, nn, kExtLdsBlock);
     stage_lds(s_leaves, ALL ? sc.bleaf : sc.fbleaf, nl, kExtLdsBlock);
     stage_lds(s_sph, ALL ? sc.sph : sc.fsph, ns, kExtLdsBlock);
     if (ALL) stage_lds(s_msph, sc.msph, nm, kExtLdsBlock);
+    stage_words(reinterpret_cast<uint32_t*>(s_fid), reinterpret_cast<const uint32_t*>(sc.fid), sc.n_fsph, kExtLdsBlock);
+    stage_words(reinterpret_cast<uint32_t*>(s_cls), reinterpret_cast<const uint32_t*>(sc.leaf_cls),
+                (sc.n_leaves + 3) / 4, kExtLdsBlock);
     __syncthreads();
-    const Tree0 t0 = ALL ? tree0_hbm(sc) : Tree0{s_nodes, s_leaves, s_sph};
+    const Tree0 t0 = ALL ? tree0_hbm(sc) : Tree0{s_nodes, s_leaves, s_sph, s_fid};
     const TreeA ta = ALL ? TreeA{s_nodes, s_leaves, s_sph, s_msph} : treeA_hbm(sc);
     const int LS = sc.lane_stack;
     for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
@@ -1236,7 +1259,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const 
                 st.tm[w] = time;
                 st.rng0[w] = g.ctr;
                 hit.h[w] = HitRec{t, leaf, 0};
-                cls = sc.leaves[leaf].mtype;
+                cls = s_cls[leaf];
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
@@ -1657,7 +1680,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
         stage_lds(s_nodes, sc.fbvh2, nn, 256);
         stage_lds(s_leaves, sc.fbleaf, nl, 256);
         stage_lds(s_sph, sc.fsph, ns, 256);
-        t0 = Tree0{s_nodes, s_leaves, s_sph};
+        t0 = Tree0{s_nodes, s_leaves, s_sph, sc.fid};
         __syncthreads();
     }
     stage_perlin(sc, P);
