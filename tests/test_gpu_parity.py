@@ -237,6 +237,46 @@ def _moving_mix_scene(nx, ny):
     return g.make_scene(objs, scenes.camera_for(nx, ny), g.sky_color)
 
 
+def _static_cover_scene(nx, ny):
+    """The cover scene with every moving sphere frozen where it starts: no
+    moving spheres, so the time-0 tree serves camera rays too (k_camera<false>)."""
+    from rtamd import scene as g
+    sc = scenes.random_scene(nx, ny)
+    objs = [g.make_sphere(o.args[0], o.args[4], o.args[5]) if o.kind == "moving_sphere" else o
+            for o in sc.obj_list]
+    return g.make_scene(objs, sc.camera, sc.sky_function)
+
+
+def _many_spheres_scene(nx, ny):
+    """2000 small spheres of all three materials: the trees outgrow the LDS
+    kernels' budget, so every launch takes the HBM-tree kernels."""
+    from rtamd import scene as g, vec as v
+    from rtamd.rng import HostStream
+    rr = HostStream(0x5EED0102)
+    mats = [g.make_lambertian(g.constant_texture(v.vec3(0.6, 0.5, 0.4))),
+            g.make_metal(g.constant_texture(v.vec3(0.8, 0.8, 0.7)), 0.2), g.make_dielectric(1.5)]
+    objs = [g.make_sphere(v.vec3(0, -1000, 0), 1000, mats[0])]
+    for i in range(2000):
+        objs.append(g.make_sphere(v.vec3(rr() * 20 - 10, rr() * 2, rr() * 20 - 10), 0.05 + 0.1 * rr(), mats[i % 3]))
+    return g.make_scene(objs, scenes.camera_for(nx, ny), g.sky_color)
+
+
+@pytest.mark.parametrize("make", [_static_cover_scene, _many_spheres_scene])
+def test_kernel_paths_match_flat_list_bitwise(gpu_ctx, monkeypatch, make):
+    """Scenes that take the other closest-hit paths (time-0 tree for camera
+    rays; trees too big for LDS) equal the brute-force flat list bit for bit."""
+    nx, ny, spp = 48, 27, 4
+    imgs = []
+    for env in ({"RTAMD_BVH_MIN": "1000000000"}, {}):
+        monkeypatch.delenv("RTAMD_BVH_MIN", raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        a = np.zeros(nx * ny * 3)
+        gpu.render_host(make(nx, ny), nx, ny, 0, spp, SEED, a)
+        imgs.append(a)
+    assert np.array_equal(imgs[0], imgs[1])
+
+
 @pytest.mark.parametrize("make", [scenes.random_scene, _moving_mix_scene])
 def test_time0_bvh_matches_all_times_bvh_bitwise(gpu_ctx, monkeypatch, make):
     """Scattered rays (time 0) traverse the time-0 tree with moving spheres

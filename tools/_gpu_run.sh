@@ -1,5 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
-RTAMD_DEBUG_COUNTS=1 RTAMD_LIB=scheme-raytrace_amd/rtamd/librtamd_stats.so timeout -k 10 200 python tools/trav_stats.py cover 2 > gpurun_out/trav_stats.json 2> gpurun_out/trav_stats.err || { tail gpurun_out/trav_stats.err; exit 1; }
-cat gpurun_out/trav_stats.json | grep -v "^  *\"\(lane\|wave\|lanes\)"
-grep "neighbours" gpurun_out/trav_stats.err | sort | uniq -c | head
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 90 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log | cut -c1-300; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+run() { tag=$1; shift; env "$@" timeout -k 10 300 python bench.py --spp 256 --steps 2 --warmup 1 --no-cpu-baseline --no-isolated > gpurun_out/bench_$tag.log 2>&1 || exit 1
+  python -c "import json,sys; d=json.loads(open('gpurun_out/bench_$tag.log').read().strip().splitlines()[-1]); print('$tag', d['value'], d['ms_per_step'], d['ms_extend_per_step'], d['ms_shade_per_step'], d['ms_finish_per_step'])"; }
+L=scheme-raytrace_amd/rtamd
+run pf_l1 RTAMD_LANES=1
+run cw5_l1 RTAMD_LANES=1 RTAMD_LIB=$L/librtamd_cw5.so
+run pf X=1
