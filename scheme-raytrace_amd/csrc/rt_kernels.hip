@@ -36,8 +36,11 @@ namespace rtamd {
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
                                          uint32_t k0, uint32_t k1) {
+#ifndef RT_PHILOX_ROUNDS
+#define RT_PHILOX_ROUNDS 10     // A/B builds only; 10 is the stream's definition
+#endif
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
         if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
         const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
@@ -1655,7 +1658,7 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
-template <int F>
+template <int F, bool PN, bool LSM>
 __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
@@ -1683,7 +1686,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
         t0 = Tree0{s_nodes, s_leaves, s_sph, sc.fid};
         __syncthreads();
     }
-    stage_perlin(sc, P);
+    stage_perlin<PN>(sc, P);
     // Persistent lanes: a lane whose path ended takes the next unstarted one
     // (one atomic per wave per refill), so a wave is not held by its longest
     // path while its other lanes idle.  tail_ctl[0] counts segments,
@@ -1720,7 +1723,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             v3 L;
             bool cont = false;
             if (leaf < 0) L = sky_radiance(sc, p.d);
-            else cont = shade_hit<-1>(sc, P, rp, p, t, leaf, L, sc.leaves);
+            else cont = shade_hit<-1, PN, LSM>(sc, P, rp, p, t, leaf, L, sc.leaves);
             if (!cont) { write_sample(rp, p, L); active = false; }
         }
     }
@@ -1904,15 +1907,25 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
                         (size_t)sc.n_fsph * sizeof(SphereRec);
     const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
     if (tree0_lds) lds += tree;
-#define RT_FINISH_F(F) \
-    hipLaunchKernelGGL((k_finish<F>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth0)
+#define RT_FINISH_F(F) RT_FINISH(F, true, true)
+#define RT_FINISH(F, PN, LS) \
+    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth0)
+    // the plain-sphere feature set also gets Perlin / light-mixture specialisations:
+    // the tail kernel carries every material's code, so dropping the unused ones
+    // trims its register file
+    const bool pn = sc.has_noise_tex != 0;
+    const bool ls = sc.light.type != LIGHT_OFF;
     switch (scene_features(sc)) {
-    case 0: RT_FINISH_F(0); break;
+    case 0:
+        if (pn) { if (ls) RT_FINISH(0, true, true); else RT_FINISH(0, true, false); }
+        else { if (ls) RT_FINISH(0, false, true); else RT_FINISH(0, false, false); }
+        break;
     case 1: RT_FINISH_F(1); break;
     case 2: RT_FINISH_F(2); break;
     default: RT_FINISH_F(3); break;
     }
 #undef RT_FINISH_F
+#undef RT_FINISH
     return hipGetLastError();
 }
 #ifdef RT_STATS
