@@ -359,6 +359,18 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
     return true;
 }
 
+#ifdef RT_STATS
+// traversal statistics (stats builds only): rays, node visits, leaf visits,
+// sphere tests, moving-sphere tests, lane inner / outer loop iterations,
+// waves, wave-max inner / outer iterations, lanes; [0..10] all-times tree,
+// [16..26] time-0 tree; curve trees: [11] rays, [12] node visits, [13] leaf
+// visits, [14] queued curve candidates, [15] root-cull survivors, [27] flushes
+__device__ unsigned long long g_stats[32];
+#define RT_STAT(k, v) atomicAdd(&g_stats[k], (unsigned long long)(v))
+#else
+#define RT_STAT(k, v) ((void)0)
+#endif
+
 // ------------------------------------------------- curve candidate batching
 // Curve tests are long and their length varies per (ray, curve), so testing
 // a curve in the lane that reached its BVH leaf leaves most of the wave idle.
@@ -406,6 +418,9 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
         const unsigned long long m = __ballot(keep);
         if (keep) W.sv[svn + lanes_below(m)] = e;
         svn += (uint32_t)__popcll(m);
+#ifdef RT_STATS
+        if (rank == 0) RT_STAT(15, __popcll(m));
+#endif
     }
     wave_sync();
     return svn;
@@ -487,17 +502,6 @@ __device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, con
     hl = one(0, tl);
     hr = one(1, tr);
 }
-
-#ifdef RT_STATS
-// traversal statistics (stats builds only): rays, node visits, leaf visits,
-// sphere tests, moving-sphere tests, lane inner / outer loop iterations,
-// waves, wave-max inner / outer iterations, lanes; [0..10] all-times tree,
-// [16..26] time-0 tree
-__device__ unsigned long long g_stats[32];
-#define RT_STAT(k, v) atomicAdd(&g_stats[k], (unsigned long long)(v))
-#else
-#define RT_STAT(k, v) ((void)0)
-#endif
 
 // FROZEN: the time-0 tree (DevScene::fbvh2), whose leaves hold plain sphere
 // records (moving spheres at center(0)); otherwise the all-times tree.
@@ -636,9 +640,15 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
     bool trav = true;
     int pb = 0, pe = 0;                         // this lane's curves still to queue
     uint32_t qn = 0, svn = 0;                   // queued candidates, survivors awaiting subdivision
+#ifdef RT_STATS
+    uint32_t n_node = 0, n_leaf = 0, n_cand = 0, n_flush = 0;
+#endif
     for (;;) {
         if (pb >= pe && trav) {                 // lanes with curves pending only queue them below
             if (node >= 0) {
+#ifdef RT_STATS
+                ++n_node;
+#endif
                 const BvhNode2 N = sc.bvh2[node];
                 const float tcap = f32_up(closest * tscale);
                 float tl, tr;
@@ -671,6 +681,9 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                     sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
                 }
                 pb = L.bb; pe = L.bb + L.bn;
+#ifdef RT_STATS
+                ++n_leaf; n_cand += (uint32_t)L.bn;
+#endif
                 if (sp == 0) {
                     trav = false;
                 } else {
@@ -689,6 +702,9 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
         }
         const bool more = __ballot(trav || pb < pe) != 0ull;
         if (qn >= 64u || (!more && (qn > 0u || svn > 0u))) {
+#ifdef RT_STATS
+            ++n_flush;
+#endif
             W.cl[lane] = closest;
             wave_sync();
             svn = bez_stage_a(sc, W, qn, svn);
@@ -710,6 +726,10 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
         }
         if (!more) break;
     }
+#ifdef RT_STATS
+    RT_STAT(11, 1); RT_STAT(12, n_node); RT_STAT(13, n_leaf); RT_STAT(14, n_cand);
+    if (lane == (uint32_t)__ffsll((long long)__ballot(1)) - 1u) RT_STAT(27, n_flush);
+#endif
 }
 
 // ---------------------------------------------------------- closest hit

@@ -42,7 +42,13 @@ def main():
                           "lane_inner_iters": buf[o + 5] / n, "lane_outer_iters": buf[o + 6] / n,
                           "wave_max_inner_iters": buf[o + 8] / w, "wave_max_outer_iters": buf[o + 9] / w,
                           "lanes_per_wave": buf[o + 10] / w}
+        if buf[11]:
+            n = buf[11]
+            r["curves"] = {"queries": n, "nodes": buf[12] / n, "leaves": buf[13] / n, "candidates": buf[14] / n,
+                           "root_survivors": buf[15] / n, "flushes_per_wave_query": buf[27] * 64.0 / n}
         out[mode] = r
+        if scene_name.startswith("curves"):
+            break
     print(json.dumps(out, indent=1))
 
 
