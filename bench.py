@@ -43,6 +43,27 @@ def extend_bytes(segments, paths):
     return EXTEND_BYTES_PER_SEGMENT * segments + EXTEND_BYTES_PER_PATH * paths
 
 
+# Algorithmic HBM bytes of the wavefront shade phase (the per-material k_shade
+# launches of an iteration): a shaded hit reads its queue entry (4), hit record
+# (16) and ray record (48), plus the camera ray's time and draw counter (12)
+# at depth 0 or the path record (40) deeper; a survivor writes ray + path
+# records (88), a path that ends at the hit writes its sample colour (24).
+def shade_bytes(hits_d0, hits, survivors):
+    return (80 * hits_d0 + 108 * hits + 88 * survivors + 24 * (hits_d0 + hits - survivors))
+
+
+def shade_roofline(st, note):
+    if not st or not st.extend_launches or st.ms_shade <= 0 or not (st.shade_hits_d0 + st.shade_hits):
+        return None
+    b = shade_bytes(st.shade_hits_d0, st.shade_hits, st.shade_survivors)
+    ach = b / (st.ms_shade * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": "k_shade<material> (one iteration's launches)",
+            "bytes_per_launch": round(b / st.extend_launches),
+            "hits_per_launch": round((st.shade_hits_d0 + st.shade_hits) / st.extend_launches),
+            "avg_launch_ms": round(st.ms_shade / st.extend_launches, 4), "note": note}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -225,6 +246,7 @@ def main():
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
             "roofline": roof, "roofline_isolated": roof_iso, "valu": valu,
+            "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated"),
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),

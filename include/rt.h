@@ -161,6 +161,9 @@ typedef struct rt_stats {
     uint32_t reserved;
     double   ms_finish;       /* summed device time of the tail kernel */
     uint64_t finish_paths;    /* paths handed to the tail kernel */
+    uint64_t shade_hits_d0;   /* camera-ray hits shaded by the wavefront shade kernels */
+    uint64_t shade_hits;      /* deeper hits shaded by the wavefront shade kernels */
+    uint64_t shade_survivors; /* paths the shade kernels wrote on to the next iteration */
 } rt_stats;
 int rt_get_stats(int scene, rt_stats* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */

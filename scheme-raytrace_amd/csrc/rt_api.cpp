@@ -1104,7 +1104,8 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
                                 (uint32_t)shard_cap, L.depth == 0, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));
-        HIPCHK(hipMemcpyAsync(L.h_counts + L.depth * kCountsPerIter, surv, kShards * kCntStride * sizeof(uint32_t),
+        (void)surv;                                  // the whole row: queue counts (statistics) + survivors
+        HIPCHK(hipMemcpyAsync(L.h_counts + L.depth * kCountsPerIter, cnt, kCountsPerIter * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, L.stream));
         HIPCHK(hipEventRecord(L.ev_cnt, L.stream));
         L.state = Lane::RUNNING;
@@ -1123,12 +1124,17 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         s->stats.extend_rays += L.n;
         s->stats.segments += L.n;
         if ((uint32_t)L.depth > s->stats.max_depth_seen) s->stats.max_depth_seen = (uint32_t)L.depth;
+        const uint32_t* row = L.h_counts + L.depth * kCountsPerIter;
         uint32_t n = 0;
         for (int x = 0; x < kShards; ++x) {
-            const uint32_t c_x = L.h_counts[L.depth * kCountsPerIter + x * kCntStride];
+            const uint32_t c_x = row[4 * kShards * kCntStride + x * kCntStride];
             if (c_x > shard_cap) return fail("internal: shard overflow");
             n += c_x;
         }
+        uint64_t hits = 0;
+        for (int k = 0; k < 4 * kShards; ++k) hits += row[k * kCntStride];
+        (L.depth == 0 ? s->stats.shade_hits_d0 : s->stats.shade_hits) += hits;
+        s->stats.shade_survivors += n;
         L.view = QView{L.counts.as<uint32_t>() + L.depth * kCountsPerIter + 4 * kShards * kCntStride,
                        (uint32_t)shard_cap};
         std::swap(L.cur, L.nxt);

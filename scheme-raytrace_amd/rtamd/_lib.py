@@ -35,6 +35,9 @@ class RtStats(ctypes.Structure):
         ("reserved", ctypes.c_uint32),
         ("ms_finish", ctypes.c_double),
         ("finish_paths", ctypes.c_uint64),
+        ("shade_hits_d0", ctypes.c_uint64),
+        ("shade_hits", ctypes.c_uint64),
+        ("shade_survivors", ctypes.c_uint64),
     ]
 
 
