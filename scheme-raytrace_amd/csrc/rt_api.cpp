@@ -22,7 +22,7 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, hipStream_t);
+                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, unsigned int*, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, bool,
                         hipStream_t);
@@ -1094,7 +1094,8 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
                                      cnt, s->ext_lds_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
         else
             HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
-                                 L.depth == 0, L.stream));
+                                 L.depth == 0, reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1),
+                                 L.stream));
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
         for (int mt = 0; mt < 4; ++mt) {

@@ -364,7 +364,8 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
 // sphere tests, moving-sphere tests, lane inner / outer loop iterations,
 // waves, wave-max inner / outer iterations, lanes; [0..10] all-times tree,
 // [16..26] time-0 tree; curve trees: [11] rays, [12] node visits, [13] leaf
-// visits, [14] queued curve candidates, [15] root-cull survivors, [27] flushes
+// visits, [14] queued curve candidates, [15] root-cull survivors, [27] flushes,
+// [28] wave loop iterations, [29] waves, [30] lanes
 __device__ unsigned long long g_stats[32];
 #define RT_STAT(k, v) atomicAdd(&g_stats[k], (unsigned long long)(v))
 #else
@@ -392,6 +393,7 @@ struct BezWave {
     uint32_t q[kBezQ];              // candidates: curve << 6 | owner
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
+    uint32_t done[64];              // persistent kernel: owner's candidates resolved so far
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -404,6 +406,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 // Stage A: root cull of the qn queued candidates; survivors are appended to
 // the survivor list (svn entries already there).  Returns the new count.
 // Every active lane calls it with the same arguments.
+template <bool TRACK = false>
 __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, const uint32_t qn, uint32_t svn) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
@@ -414,6 +417,7 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
         if (i < qn) {
             e = W.q[i];
             keep = bez_root_passes(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
+            if (TRACK && !keep) atomicAdd(&W.done[e & 63u], 1u);
         }
         const unsigned long long m = __ballot(keep);
         if (keep) W.sv[svn + lanes_below(m)] = e;
@@ -429,6 +433,7 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
 // Stage B: full subdivision of the first nb survivors, one per lane, then per
 // owner the smallest z (ties: smallest curve index) into hz / hid; the
 // remaining svn - nb survivors move to the front.
+template <bool TRACK = false>
 __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
@@ -453,6 +458,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             const uint32_t e = W.sv[i], o = e & 63u;
             if (W.sz[i] == W.hz[o]) atomicMin(&W.hid[o], e >> 6);
         }
+        if (TRACK && i < nb) atomicAdd(&W.done[W.sv[i] & 63u], 1u);
     }
     wave_sync();
     const uint32_t rest = svn - nb;             // < nact <= 64, disjoint from [0, rest) only if nb >= rest
@@ -641,9 +647,12 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
     int pb = 0, pe = 0;                         // this lane's curves still to queue
     uint32_t qn = 0, svn = 0;                   // queued candidates, survivors awaiting subdivision
 #ifdef RT_STATS
-    uint32_t n_node = 0, n_leaf = 0, n_cand = 0, n_flush = 0;
+    uint32_t n_node = 0, n_leaf = 0, n_cand = 0, n_flush = 0, n_iter = 0;
 #endif
     for (;;) {
+#ifdef RT_STATS
+        ++n_iter;
+#endif
         if (pb >= pe && trav) {                 // lanes with curves pending only queue them below
             if (node >= 0) {
 #ifdef RT_STATS
@@ -728,7 +737,9 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
     }
 #ifdef RT_STATS
     RT_STAT(11, 1); RT_STAT(12, n_node); RT_STAT(13, n_leaf); RT_STAT(14, n_cand);
-    if (lane == (uint32_t)__ffsll((long long)__ballot(1)) - 1u) RT_STAT(27, n_flush);
+    if (lane == (uint32_t)__ffsll((long long)__ballot(1)) - 1u) {
+        RT_STAT(27, n_flush); RT_STAT(28, n_iter); RT_STAT(29, 1); RT_STAT(30, __popcll(__ballot(1)));
+    }
 #endif
 }
 
@@ -865,13 +876,81 @@ __device__ __forceinline__ Tree0 tree0_hbm(const DevScene& sc) { return Tree0{sc
 struct TreeA { const BvhNode2* nodes; const BvhLeaf* leaves; const SphereRec* sph; const MSphereRec* msph; };
 __device__ __forceinline__ TreeA treeA_hbm(const DevScene& sc) { return TreeA{sc.bvh2, sc.bleaf, sc.sph, sc.msph}; }
 
+// One non-BVH group of hit-obj-list (geometry.scm:33-50): its primitives in
+// list order against the shrinking closest.
+template <int F>
+__device__ __forceinline__ void group_closest(const DevScene& sc, const Group& G, const v3 o0, const v3 d0,
+                                              const double time, double& closest, int32_t& best, Rng* rng) {
+    constexpr bool BEZ = (F & kFeatCurves) != 0;
+    constexpr bool MED = (F & kFeatExtra) != 0;
+    v3 o = o0, d = d0;
+    if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
+    const int32_t base = sc.leaf_base[G.type];
+    if (G.type == LEAF_SPHERE) {                       // geometry.scm:146-171
+        const double a = dot(d, d);
+        for (int s = G.begin; s < G.end; ++s) {
+            const SphereRec S = sc.sph[s];
+            sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, base + s, closest, best);
+        }
+    } else if (G.type == LEAF_MSPHERE) {               // geometry.scm:177-208
+        const double a = dot(d, d);
+        double last_t0 = 0.0, last_den = 0.0, frac = 0.0;
+        bool have = false;
+        for (int s = G.begin; s < G.end; ++s) {
+            const MSphereRec S = sc.msph[s];
+            if (!have || S.t0 != last_t0 || S.den != last_den) {   // uniform branch
+                frac = (time - S.t0) / S.den;
+                last_t0 = S.t0; last_den = S.den; have = true;
+            }
+            const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+            sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
+        }
+    } else if (G.type == LEAF_KLEIN) {                 // geometry.scm:645-673
+        if (MED) {
+            for (int s = G.begin; s < G.end; ++s) {
+                double t;
+                if (klein_test(sc.klein[s], o, d, closest, t)) { closest = t; best = base + s; }
+            }
+        }
+    } else if (G.type == LEAF_MEDIUM) {                // geometry.scm:545-578
+        if (MED) {
+            for (int s = G.begin; s < G.end; ++s) {
+                double t;
+                if (medium_test(sc, sc.med[s], o0, d0, d, time, closest, *rng, t)) { closest = t; best = base + s; }
+            }
+        }
+    } else if (G.type == LEAF_BEZIER) {                // bezier.scm:176-214
+        if (BEZ) {
+            BezRay R;
+            bez_ray(o, d, R);
+            for (int s = G.begin; s < G.end; ++s) {
+                double t;
+                if (bezier_test(sc.bez[s], R, closest, t)) { closest = t; best = base + s; }
+            }
+        }
+    } else {                                            // geometry.scm:376-431
+        // XY: k on z, (a,b) = (x,y); XZ: k on y, (x,z); YZ: k on x, (y,z)
+        double ok, dk, oa, da, ob, db;
+        if (G.type == LEAF_RECT_XY) { ok = o.z; dk = d.z; oa = o.x; da = d.x; ob = o.y; db = d.y; }
+        else if (G.type == LEAF_RECT_XZ) { ok = o.y; dk = d.y; oa = o.x; da = d.x; ob = o.z; db = d.z; }
+        else { ok = o.x; dk = d.x; oa = o.y; da = d.y; ob = o.z; db = d.z; }
+        for (int s = G.begin; s < G.end; ++s) {
+            const RectRec R = sc.rect[s];
+            const double t = (R.k - ok) / dk;
+            if (t < kTmin || t > closest) continue;
+            const double A = oa + t * da, Bv = ob + t * db;
+            if (A < R.a0 || A > R.a1 || Bv < R.b0 || Bv > R.b1) continue;
+            closest = t; best = base + s;
+        }
+    }
+}
+
 template <int F, class SE = uint32_t>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, const v3 d0,
                                                const double time, double& closest, SE* lstk,
                                                const int lmax, BezWave* bw, Rng* rng, const Tree0 t0,
                                                const TreeA ta) {
     constexpr bool BEZ = (F & kFeatCurves) != 0;
-    constexpr bool MED = (F & kFeatExtra) != 0;
     int32_t best = -1;
     closest = kTmax;
     for (int g = 0; g < sc.n_groups; ++g) {
@@ -886,66 +965,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
                                          ta.sph, ta.msph);
             continue;
         }
-        v3 o = o0, d = d0;
-        if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
-        const int32_t base = sc.leaf_base[G.type];
-        if (G.type == LEAF_SPHERE) {                       // geometry.scm:146-171
-            const double a = dot(d, d);
-            for (int s = G.begin; s < G.end; ++s) {
-                const SphereRec S = sc.sph[s];
-                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, base + s, closest, best);
-            }
-        } else if (G.type == LEAF_MSPHERE) {               // geometry.scm:177-208
-            const double a = dot(d, d);
-            double last_t0 = 0.0, last_den = 0.0, frac = 0.0;
-            bool have = false;
-            for (int s = G.begin; s < G.end; ++s) {
-                const MSphereRec S = sc.msph[s];
-                if (!have || S.t0 != last_t0 || S.den != last_den) {   // uniform branch
-                    frac = (time - S.t0) / S.den;
-                    last_t0 = S.t0; last_den = S.den; have = true;
-                }
-                const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
-            }
-        } else if (G.type == LEAF_KLEIN) {                 // geometry.scm:645-673
-            if (MED) {
-                for (int s = G.begin; s < G.end; ++s) {
-                    double t;
-                    if (klein_test(sc.klein[s], o, d, closest, t)) { closest = t; best = base + s; }
-                }
-            }
-        } else if (G.type == LEAF_MEDIUM) {                // geometry.scm:545-578
-            if (MED) {
-                for (int s = G.begin; s < G.end; ++s) {
-                    double t;
-                    if (medium_test(sc, sc.med[s], o0, d0, d, time, closest, *rng, t)) { closest = t; best = base + s; }
-                }
-            }
-        } else if (G.type == LEAF_BEZIER) {                // bezier.scm:176-214
-            if (BEZ) {
-                BezRay R;
-                bez_ray(o, d, R);
-                for (int s = G.begin; s < G.end; ++s) {
-                    double t;
-                    if (bezier_test(sc.bez[s], R, closest, t)) { closest = t; best = base + s; }
-                }
-            }
-        } else {                                            // geometry.scm:376-431
-            // XY: k on z, (a,b) = (x,y); XZ: k on y, (x,z); YZ: k on x, (y,z)
-            double ok, dk, oa, da, ob, db;
-            if (G.type == LEAF_RECT_XY) { ok = o.z; dk = d.z; oa = o.x; da = d.x; ob = o.y; db = d.y; }
-            else if (G.type == LEAF_RECT_XZ) { ok = o.y; dk = d.y; oa = o.x; da = d.x; ob = o.z; db = d.z; }
-            else { ok = o.x; dk = d.x; oa = o.y; da = d.y; ob = o.z; db = d.z; }
-            for (int s = G.begin; s < G.end; ++s) {
-                const RectRec R = sc.rect[s];
-                const double t = (R.k - ok) / dk;
-                if (t < kTmin || t > closest) continue;
-                const double A = oa + t * da, Bv = ob + t * db;
-                if (A < R.a0 || A > R.a1 || Bv < R.b0 || Bv > R.b1) continue;
-                closest = t; best = base + s;
-            }
-        }
+        group_closest<F>(sc, G, o0, d0, time, closest, best, rng);
     }
     return best;
 }
@@ -1111,6 +1131,219 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     }
     const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
     if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+}
+
+// Wave-level append into the sharded material queues (block_append's layout:
+// class c, shard x -> counter (c * kShards + x), slot x * shard_cap + rank)
+// for kernels whose lanes finish at different loop iterations.  One atomic
+// per distinct (class, shard) among the wave's finishing lanes.
+__device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t shard, uint32_t* __restrict__ counts,
+                                                const uint32_t shard_cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    bool pending = cls >= 0;
+    const uint32_t key = pending ? (uint32_t)cls * kShards + shard : 0u;
+    uint32_t slot = 0;
+    unsigned long long m = __ballot(pending);
+    while (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        const uint32_t K = (uint32_t)__shfl((int)key, leader, 64);
+        const bool mine = pending && key == K;
+        const unsigned long long mk = __ballot(mine);
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(counts + K * kCntStride, (uint32_t)__popcll(mk));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (mine) { slot = (K % kShards) * shard_cap + base + lanes_below(mk); pending = false; }
+        m = __ballot(pending);
+    }
+    return slot;
+}
+
+// =====================================================================
+// k_extend_curves — closest hit for scenes whose world BVH holds curves
+// (bezier.scm), persistent: a lane whose ray is resolved takes the next one
+// (one claim atomic per wave), so a wave is not held by its longest ray
+// (stats build: a wave looped 417 times for 77 steps per ray on average).
+// Same traversal, candidate batching and group order as closest_hit /
+// bvh_closest_curves; a ray finishes once its traversal has ended and every
+// curve candidate it queued has been resolved by a batch (W.done).
+// =====================================================================
+__global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const RenderParams rp,
+                                                       const PathState st, const QView in, uint32_t n, HitBuf hit,
+                                                       uint32_t* __restrict__ queues, uint32_t qstride,
+                                                       uint32_t shard_cap, uint32_t* __restrict__ counts,
+                                                       const bool depth0, unsigned int* __restrict__ claim) {
+    constexpr int F = kFeatCurves;
+    extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
+    __shared__ BezWave s_bw[4];
+    BezWave& W = s_bw[threadIdx.x >> 6];
+    uint32_t* lstk = s_lstack + threadIdx.x;
+    const int lmax = sc.lane_stack;
+    const uint32_t stride = blockDim.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const QMap qm = qmap(in);
+    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
+    int gb = 0;                                     // the world BVH group (commit_scene builds at most one)
+    while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
+    bool active = false, exhausted = false, trav = false;
+    uint32_t k = 0, i = 0, queued = 0;
+    v3 o = mk(0.0, 0.0, 0.0), d = o;
+    double tm = 0.0, a = 0.0, tscale = 1.0, closest = kTmax;
+    int32_t best = -1, node = 0;
+    BoxRay br{};
+    BvhNode2 N{};                                   // the lane's next node, loaded one iteration ahead
+    int sp = 0, pb = 0, pe = 0;
+    uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
+#ifdef RT_STATS
+    uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
+#endif
+    for (;;) {
+#ifdef RT_STATS
+        ++st_iter;
+        if (active && trav && pb >= pe) ++st_steps;
+        if (active) ++st_busy;
+        if (active && !trav && pb >= pe) ++st_wait;
+#endif
+        // 1. rays whose traversal ended and whose curves are all resolved: the
+        //    groups after the BVH, then miss (sky) or hit + material queue
+        int cls = -1;
+        if (active && !trav && pb >= pe && W.done[lane] == queued) {
+            for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+            if (best < 0) {
+                const v3 L = sky_radiance(sc, d);
+                if (depth0) {                                // throughput 1: (* 1 x) = x
+                    rp.sb[i] = 1.0 * L.x;
+                    rp.sb[rp.B + i] = 1.0 * L.y;
+                    rp.sb[2u * rp.B + i] = 1.0 * L.z;
+                } else {
+                    const PathRec P = st.path[i];
+                    rp.sb[P.wid] = P.tr * L.x;
+                    rp.sb[rp.B + P.wid] = P.tg * L.y;
+                    rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
+                }
+            } else {
+                hit.h[i] = HitRec{closest, best, 0};
+                cls = sc.leaves[best].mtype;
+            }
+            active = false;
+        }
+        const uint32_t slot = wave_append(cls, (k >> 8) & (uint32_t)(kShards - 1), counts, shard_cap);
+        if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+        // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
+        const unsigned long long need = __ballot(!active);
+        if (need && !exhausted) {
+            const uint32_t cnt = (uint32_t)__popcll(need);
+            const int leader = __ffsll((long long)need) - 1;
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(claim, cnt);
+            base = (uint32_t)__shfl((int)base, leader, 64);
+            if (base + cnt >= n) exhausted = true;
+            if (!active) {
+                const uint32_t kk = base + lanes_below(need);
+                if (kk < n) {
+                    k = kk;
+                    i = qphys(qm, kk);
+                    const RayRec R = st.ray[i];
+                    o = mk(R.ox, R.oy, R.oz);
+                    d = mk(R.dx, R.dy, R.dz);
+                    tm = depth0 ? st.tm[i] : 0.0;
+                    closest = kTmax;
+                    best = -1;
+                    for (int g = 0; g < gb; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+                    a = dot(d, d);
+                    br = box_ray(o, d);
+                    tscale = fmax(1.0, 1.0 / sqrt(a));
+                    bez_ray(o, d, W.ray[lane]);
+                    W.done[lane] = 0u;
+                    queued = 0u;
+                    sp = 0; node = sc.bvh2_root; trav = gb < sc.n_groups; pb = pe = 0;
+                    if (trav && node >= 0) N = sc.bvh2[node];
+                    active = true;
+                }
+            }
+        }
+        if (__ballot(active) == 0ull) break;         // every queued candidate has been resolved
+        // 3. one BVH step (bvh_closest_curves)
+        if (active && trav && pb >= pe) {
+            if (node >= 0) {
+                const float tcap = f32_up(closest * tscale);
+                float tl, tr;
+                bool hl, hr;
+                node_hit(N, br, tcap, hl, hr, tl, tr);
+                if (hl && hr) {
+                    const bool lfirst = tl <= tr;
+                    if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
+                    node = lfirst ? N.l : N.r;
+                } else if (hl) {
+                    node = N.l;
+                } else if (hr) {
+                    node = N.r;
+                } else if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
+            } else {
+                const BvhLeaf L = sc.bleaf[~node];
+                for (int s = L.sb; s < L.sb + L.sn; ++s) {
+                    const SphereRec S = sc.sph[s];
+                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                }
+                for (int s = L.mb; s < L.mb + L.mn; ++s) {
+                    const MSphereRec S = sc.msph[s];
+                    const double frac = (tm - S.t0) / S.den;
+                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                }
+                pb = L.bb; pe = L.bb + L.bn;
+                if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
+            }
+        }
+        // the next node's record, in flight while the batches below run
+        if (active && trav && node >= 0) N = sc.bvh2[node];
+        // 4. queue this step's curve candidates (at most 2 per lane)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool has = active && pb < pe;
+            const unsigned long long m = __ballot(has);
+            if (has) { W.q[qn + lanes_below(m)] = ((uint32_t)pb << 6) | lane; ++pb; ++queued; }
+            qn += (uint32_t)__popcll(m);
+        }
+        // 5. batches: root culls at 64 queued candidates, subdivisions in
+        //    multiples of 64 (everything once no lane can add candidates)
+        const bool more = __ballot(active && (trav || pb < pe)) != 0ull;
+        if (qn >= 64u || (!more && (qn > 0u || svn > 0u))) {
+#ifdef RT_STATS
+            ++st_flush;
+#endif
+            W.cl[lane] = closest;
+            wave_sync();
+            svn = bez_stage_a<true>(sc, W, qn, svn);
+            qn = 0;
+            const uint32_t nb = more ? svn - svn % 64u : svn;
+            if (nb > 0u) {
+                W.hz[lane] = INFINITY;
+                W.hid[lane] = 0xFFFFFFFFu;
+                wave_sync();
+                bez_stage_b<true>(sc, W, nb, svn);
+                svn -= nb;
+                if (active && W.hid[lane] != 0xFFFFFFFFu && W.hz[lane] <= closest) {   // z <= the t-max it was tested with
+                    closest = W.hz[lane];
+                    best = bz + (int32_t)W.hid[lane];
+                }
+                wave_sync();
+            }
+        }
+    }
+#ifdef RT_STATS
+    RT_STAT(20, st_steps); RT_STAT(21, st_busy); RT_STAT(22, st_wait);
+    if (lane == 0u) { RT_STAT(23, st_iter); RT_STAT(24, 1); RT_STAT(25, st_flush); }
+#endif
 }
 
 #ifndef RT_EXTLDS_BLOCK
@@ -1798,11 +2031,37 @@ static uint32_t finish_blocks() {            // persistent tail grid (RTAMD_FINI
 static int scene_features(const DevScene& sc) {
     return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
 }
+static uint32_t curve_blocks() {            // cap on the persistent curve grid (RTAMD_CURVE_BLOCKS; 0 = per-ray k_extend)
+    static const uint32_t v = [] {
+        const char* e = std::getenv("RTAMD_CURVE_BLOCKS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
+    }();
+    return v;
+}
 hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
-                         uint32_t* counts, bool depth0, hipStream_t s) {
+                         uint32_t* counts, bool depth0, unsigned int* claim, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+    if (scene_features(sc) == kFeatCurves && sc.bvh_has_bez && claim && curve_blocks() > 0) {
+        // resident blocks only: later blocks would find the rays claimed
+        static size_t occ_lds = ~(size_t)0;
+        static uint32_t occ_blocks = 0;
+        if (occ_lds != lds) {
+            int per_cu = 0, dev = 0, cus = 0;
+            HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_curves, 256, lds));
+            HIP_RETURN_IF(hipGetDevice(&dev));
+            HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            occ_blocks = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+            occ_lds = lds;
+        }
+        uint32_t pb = blocks < occ_blocks ? blocks : occ_blocks;
+        if (pb > curve_blocks()) pb = curve_blocks();
+        HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
+        hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), lds, s, sc, rp, st, in, n, hit, queues, qstride,
+                           shard_cap, counts, depth0, claim);
+        return hipGetLastError();
+    }
 #define RT_EXTEND_F(F)                                                                                      \
     hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit, queues,     \
                        qstride, shard_cap, counts, depth0)

@@ -45,7 +45,14 @@ def main():
         if buf[11]:
             n = buf[11]
             r["curves"] = {"queries": n, "nodes": buf[12] / n, "leaves": buf[13] / n, "candidates": buf[14] / n,
-                           "root_survivors": buf[15] / n, "flushes_per_wave_query": buf[27] * 64.0 / n}
+                           "root_survivors": buf[15] / n, "flushes_per_wave_query": buf[27] * 64.0 / n,
+                           "wave_loop_iters": buf[28] / max(1, buf[29]), "lanes_per_wave": buf[30] / max(1, buf[29]),
+                           "lane_steps": (buf[12] + buf[13]) / n}
+        if buf[24]:
+            w = buf[24]
+            r["curves_persistent"] = {"waves": w, "wave_iters": buf[23] / w, "lane_steps_per_wave_iter": buf[20] / buf[23] / 64,
+                                      "lane_busy_frac": buf[21] / buf[23] / 64, "lane_wait_frac": buf[22] / buf[23] / 64,
+                                      "flushes_per_wave": buf[25] / w}
         out[mode] = r
         if scene_name.startswith("curves"):
             break
