@@ -2032,11 +2032,8 @@ static int scene_features(const DevScene& sc) {
     return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
 }
 static uint32_t curve_blocks() {            // cap on the persistent curve grid (RTAMD_CURVE_BLOCKS; 0 = per-ray k_extend)
-    static const uint32_t v = [] {
-        const char* e = std::getenv("RTAMD_CURVE_BLOCKS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
-    }();
-    return v;
+    const char* e = std::getenv("RTAMD_CURVE_BLOCKS");  // read per launch: tests switch it inside one process
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
 }
 hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,

@@ -408,3 +408,73 @@ def test_c_example_matches_python_host(gpu_ctx, tmp_path):
     ppm_py = tmp_path / "py.ppm"
     render.write_ppm(str(ppm_py), gpu.resolve_u8(acc, nx, ny, spp), nx, ny)
     assert ppm_c.read_bytes() == ppm_py.read_bytes()
+
+
+_WAVEFRONT_SCENES = ["cover", "cover_marble", "test_scene2", "cornell", "cornell_mixture", "cornell_smoke",
+                     "bvh_sah", "cornell_bezier", "curves_small", "cornell_klein"]
+
+
+@pytest.mark.parametrize("name", _WAVEFRONT_SCENES)
+def test_wavefront_matches_tail_kernel_bitwise(gpu_ctx, monkeypatch, name):
+    """Small renders run entirely in the tail kernel (k_finish: extend + shade
+    per lane).  With the tail switched off the same render goes through the
+    wavefront kernels (k_camera / raygen, k_extend_lds / k_extend<F> /
+    k_extend_curves, the per-material k_shade queues) for every depth: the
+    two images must agree bit for bit, for every closest-hit and material
+    path the scenes reach."""
+    nx, ny, spp = 40, 24, 3
+    if name.startswith("curves") or "bezier" in name:
+        nx, ny, spp = 32, 18, 2
+    monkeypatch.delenv("RTAMD_TAIL_PATHS", raising=False)
+    monkeypatch.delenv("RTAMD_TAIL_DIV", raising=False)
+    a = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.SCENES[name](nx, ny), nx, ny, 0, spp, SEED, a)
+    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.SCENES[name](nx, ny), nx, ny, 0, spp, SEED, b)
+    assert np.isfinite(a).all()
+    assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+def test_curve_kernels_bitwise(gpu_ctx, monkeypatch):
+    """Curves, spheres and moving spheres in one world BVH between rect
+    groups, through the wavefront: the persistent curve kernel, the per-ray
+    curve kernel and the flat list give the same image bit for bit."""
+    from rtamd import scene as g, vec as v
+    from rtamd.rng import HostStream
+    nx, ny, spp = 40, 40, 2
+    rr = HostStream(0x5EED0103)
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    metal = g.make_metal(g.constant_texture(v.vec3(0.8, 0.8, 0.7)), 0.1)
+    glass = g.make_dielectric(1.5)
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(4, 4, 4)))
+    objs = [g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, white)),
+            g.make_xz_rect(0, 555, 0, 555, 0, white)]
+    objs.append(g.bezier_array(scenes.random_polyline_curves(600), 3.0, red))
+    for i in range(40):
+        c = v.vec3(60 + rr() * 430, 40 + rr() * 400, 60 + rr() * 430)
+        m = (white, metal, glass)[i % 3]
+        if i % 4 == 0:
+            objs.append(g.make_moving_sphere(c, v.vec3(c[0], c[1] + 20, c[2]), 0.0, 1.0, 15 + 10 * rr(), m))
+        else:
+            objs.append(g.make_sphere(c, 10 + 15 * rr(), m))
+    objs += [g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)),
+             g.make_yz_rect(0, 555, 0, 555, 0, red),
+             g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white))]
+    sc = g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
+    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    imgs = []
+    for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {}, {"RTAMD_CURVE_BLOCKS": "3"}):
+        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        a = np.zeros(nx * ny * 3)
+        gpu.render_host(sc, nx, ny, 0, spp, SEED, a)
+        imgs.append(a)
+    assert np.isfinite(imgs[0]).all()
+    for a in imgs[1:]:
+        assert np.array_equal(imgs[0], a), np.abs(imgs[0] - a).max()

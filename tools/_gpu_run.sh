@@ -1,12 +1,5 @@
 set -o pipefail
-O=gpurun_out/r01h
+O=gpurun_out/tests
 mkdir -p $O
 python -c "import torch, numpy" || exit 1
-bash tools/profile_round.sh r01h || exit 1
-RTAMD_LANES=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_r01h/kt_l1 -o kt -- python3 bench.py --spp 256 --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > gpurun_out/prof_r01h/kt_l1.log 2>&1 || exit 1
-timeout -k 10 400 python bench.py > $O/bench_c2.log 2>&1 || { tail -5 $O/bench_c2.log; exit 1; }
-timeout -k 10 300 python bench.py --scene cover_marble --spp 256 --no-cpu-baseline > $O/bench_c3.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py --scene cornell --nx 1024 --ny 1024 --spp 512 > $O/bench_c4.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py --scene cornell_mixture --nx 1024 --ny 1024 --spp 512 --no-cpu-baseline > $O/bench_c4m.log 2>&1 || exit 1
-timeout -k 10 300 python bench.py --scene curves --spp 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/bench_c5.log 2>&1 || exit 1
-for f in $O/bench_*.log; do python -c "import json,sys; d=json.loads([l for l in open('$f').read().splitlines() if l.startswith('{')][-1]); c=d.get('cpu_baseline') or {}; r=d.get('roofline_isolated') or {}; sh=d.get('roofline_shade_isolated') or {}; print('$f', d['value'], d['ms_per_step'], d['segments_per_path'], c.get('value'), r.get('frac'), (d.get('roofline') or {}).get('frac'), sh.get('frac'))"; done
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -k "wavefront_matches_tail or curve_kernels_bitwise" > $O/pytest_wf.log 2>&1; echo rc=$?; grep -E "PASSED|FAILED|Error|assert" $O/pytest_wf.log | head -40; tail -3 $O/pytest_wf.log
