@@ -46,10 +46,10 @@ def extend_bytes(segments, paths):
 # Algorithmic HBM bytes of the wavefront shade phase (the per-material k_shade
 # launches of an iteration): a shaded hit reads its queue entry (4), hit record
 # (16) and ray record (48), plus the camera ray's time and draw counter (12)
-# at depth 0 or the path record (40) deeper; a survivor writes ray + path
-# records (88), a path that ends at the hit writes its sample colour (24).
+# at depth 0 or the path record (32) deeper; a survivor writes ray + path
+# records (80), a path that ends at the hit writes its sample colour (24).
 def shade_bytes(hits_d0, hits, survivors):
-    return (80 * hits_d0 + 108 * hits + 88 * survivors + 24 * (hits_d0 + hits - survivors))
+    return (80 * hits_d0 + 100 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
 
 
 def shade_roofline(st, note):

@@ -24,10 +24,10 @@ hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&,
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
                          const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, unsigned int*, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
-                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, bool,
+                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t,
                         hipStream_t);
 hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         unsigned long long*, size_t, bool, hipStream_t);
+                         unsigned long long*, size_t, uint32_t, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
 hipError_t extend_lds_prepare(size_t, uint32_t*);
@@ -1076,7 +1076,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             }
             HIPCHK(hipMemsetAsync(L.seg_tail.as<unsigned long long>() + 1, 0, sizeof(unsigned long long), L.stream));
             HIPCHK(launch_finish(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, L.seg_tail.as<unsigned long long>(),
-                                 s->ext_lds ? (size_t)32 << 10 : 0, L.depth == 0, L.stream));
+                                 s->ext_lds ? (size_t)32 << 10 : 0, (uint32_t)L.depth, L.stream));
             if (fe) HIPCHK(hipEventRecord(fe->second, L.stream));
             s->stats.finish_paths += L.n;
             L.state = Lane::DONE;
@@ -1102,7 +1102,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
             if (!(mat_mask & (1 << mt))) continue;
             const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
             HIPCHK(launch_shade(mt, s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
-                                (uint32_t)shard_cap, L.depth == 0, L.stream));
+                                (uint32_t)shard_cap, (uint32_t)L.depth, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));
         (void)surv;                                  // the whole row: queue counts (statistics) + survivors

@@ -158,10 +158,13 @@ struct DevScene {
 // Records, not one array per field: a lane reads its ray with three 16-B
 // loads, and a kernel holds 4 base pointers instead of 13 (scalar registers).
 struct alignas(16) RayRec { double ox, oy, oz, dx, dy, dz; };                 // 48 B
-struct alignas(8) PathRec { double tr, tg, tb; uint32_t wid, rng, depth, pad; };   // 40 B, depth >= 1
+// depth >= 1: throughput, work id, draw counter (32 B).  The depth is not
+// stored: every path of a wavefront iteration has the iteration's depth.
+struct alignas(8) PathRec { double tr, tg, tb; uint32_t wid, rng; };
+static_assert(sizeof(PathRec) == 32, "PathRec layout");
 struct PathState {
     RayRec* ray;          // origin, direction
-    PathRec* path;        // depth >= 1: throughput, work id, draw counter, depth
+    PathRec* path;        // depth >= 1: throughput, work id, draw counter
     double* tm;           // depth 0: time
     uint32_t* rng0;       // depth 0: draw counter
 };

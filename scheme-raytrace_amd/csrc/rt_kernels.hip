@@ -983,9 +983,11 @@ __device__ __forceinline__ void wid_key(const RenderParams& rp, const uint32_t w
     pix = rp.pixlist[wid - s_rel * rp.npix];
     smp = rp.spp0 + s_rel;
 }
-// depth0: slot i of the raygen output (wid = i, throughput 1, depth 0)
+// depth 0: slot i of the raygen output (wid = i, throughput 1); deeper: the
+// path record (its depth is the iteration's, passed in)
 __device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathRegs& p, const RenderParams& rp,
-                                          const bool depth0) {
+                                          const uint32_t depth) {
+    const bool depth0 = depth == 0u;
     const RayRec R = st.ray[i];
     p.o = mk(R.ox, R.oy, R.oz);
     p.d = mk(R.dx, R.dy, R.dz);
@@ -997,14 +999,14 @@ __device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathR
         const PathRec P = st.path[i];
         p.time = 0.0;                                    // every scattered ray (Q4)
         p.T = mk(P.tr, P.tg, P.tb);
-        p.wid = P.wid; p.depth = P.depth; p.rng = P.rng;
+        p.wid = P.wid; p.depth = depth; p.rng = P.rng;
     }
     wid_key(rp, p.wid, p.pix, p.smp);
 }
 // a scattered path (depth >= 1: no time)
 __device__ __forceinline__ void store_path(const PathState& st, uint32_t k, const PathRegs& p) {
     st.ray[k] = RayRec{p.o.x, p.o.y, p.o.z, p.d.x, p.d.y, p.d.z};
-    st.path[k] = PathRec{p.T.x, p.T.y, p.T.z, p.wid, p.rng, p.depth, 0u};
+    st.path[k] = PathRec{p.T.x, p.T.y, p.T.z, p.wid, p.rng};
 }
 // path done: sample colour = T (*) L into the chunk's sample buffer
 __device__ __forceinline__ void write_sample(const RenderParams& rp, const PathRegs& p, const v3 L) {
@@ -1875,7 +1877,7 @@ template <int MAT, bool PN, bool LS, bool LL>
 __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp, const PathState in,
                                                const HitBuf hit, const uint32_t* __restrict__ queue,
                                                const QView qv, PathState out, uint32_t* __restrict__ out_counts,
-                                               uint32_t shard_cap, const bool depth0) {
+                                               uint32_t shard_cap, const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
@@ -1895,7 +1897,7 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
         PathRegs p;
         if (k < n) {
             const uint32_t i = queue[qphys(qm, k)];
-            load_path(in, i, p, rp, depth0);
+            load_path(in, i, p, rp, depth);
             v3 L;
             const HitRec H = hit.h[i];
             alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
@@ -1915,7 +1917,7 @@ template <int F, bool PN, bool LSM>
 __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
-                                                const bool depth0) {
+                                                const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
@@ -1961,7 +1963,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             if (base + cnt >= n) exhausted = true;
             if (!active) {
                 const uint32_t k = base + lanes_below(need);
-                if (k < n) { load_path(st, qphys(qm, k), p, rp, depth0); active = true; }
+                if (k < n) { load_path(st, qphys(qm, k), p, rp, depth); active = true; }
             }
         }
         if (__ballot(active) == 0ull) break;
@@ -2143,7 +2145,7 @@ static bool shade_leaves_hbm() {             // RTAMD_SHADE_LEAVES_HBM: keep the
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
-                        const PathState& out, uint32_t* out_counts, uint32_t shard_cap, bool depth0, hipStream_t s) {
+                        const PathState& out, uint32_t* out_counts, uint32_t shard_cap, uint32_t depth, hipStream_t s) {
     // grid-stride cap: each block stages the leaf records once, so fewer,
     // longer-lived blocks (2048 measured best of 1024..8192: +1.5 % C2)
     static const uint32_t max_blocks = [] {          // RTAMD_SHADE_BLOCKS (A/B)
@@ -2159,10 +2161,10 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     do {                                                                                                     \
         if (ll)                                                                                              \
             hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hit,  \
-                               queue, qv, out, out_counts, shard_cap, depth0);                               \
+                               queue, qv, out, out_counts, shard_cap, depth);                                \
         else                                                                                                 \
             hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hit,   \
-                               queue, qv, out, out_counts, shard_cap, depth0);                               \
+                               queue, qv, out, out_counts, shard_cap, depth);                                \
     } while (0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
@@ -2181,7 +2183,7 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& st, const QView& in,
-                         uint32_t n, unsigned long long* seg_count, size_t tree0_budget, bool depth0,
+                         uint32_t n, unsigned long long* seg_count, size_t tree0_budget, uint32_t depth,
                          hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
     if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
@@ -2192,7 +2194,7 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
     if (tree0_lds) lds += tree;
 #define RT_FINISH_F(F) RT_FINISH(F, true, true)
 #define RT_FINISH(F, PN, LS) \
-    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth0)
+    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth)
     // the plain-sphere feature set also gets Perlin / light-mixture specialisations:
     // the tail kernel carries every material's code, so dropping the unused ones
     // trims its register file
