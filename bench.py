@@ -52,15 +52,23 @@ def shade_bytes(hits_d0, hits, survivors):
     return (80 * hits_d0 + 100 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
 
 
-def shade_roofline(st, note):
+def shade_roofline(st, note, scene):
     if not st or not st.extend_launches or st.ms_shade <= 0 or not (st.shade_hits_d0 + st.shade_hits):
         return None
     b = shade_bytes(st.shade_hits_d0, st.shade_hits, st.shade_survivors)
     ach = b / (st.ms_shade * 1e-3) / 1e9
+    hpl = (st.shade_hits_d0 + st.shade_hits) / st.extend_launches
+    traffic = None                      # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
+    pmc = os.path.join(ROOT, "profiles", "pmc_shade.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            pm = json.load(f)
+        if pm.get("scene") == scene and pm.get("bytes_per_hit"):
+            traffic = round(pm["bytes_per_hit"] * hpl)
     return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": "k_shade<material> (one iteration's launches)",
-            "bytes_per_launch": round(b / st.extend_launches),
-            "hits_per_launch": round((st.shade_hits_d0 + st.shade_hits) / st.extend_launches),
+            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "kernel": "k_shade<material> (one iteration's launches)",
+            "bytes_per_launch": round(b / st.extend_launches), "hits_per_launch": round(hpl),
             "avg_launch_ms": round(st.ms_shade / st.extend_launches, 4), "note": note}
 
 
@@ -163,6 +171,7 @@ def main():
     ms_ext = ms_shade = ms_fin = 0.0
     launches = 0
     tail_segs = 0
+    sh_d0 = sh = sh_surv = 0
     for _ in range(a.steps):
         s = step()
         segs += s.segments
@@ -172,6 +181,9 @@ def main():
         launches += s.extend_launches
         ms_fin += s.ms_finish
         tail_segs += s.segments - s.extend_rays
+        sh_d0 += s.shade_hits_d0
+        sh += s.shade_hits
+        sh_surv += s.shade_survivors
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -246,13 +258,15 @@ def main():
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
             "roofline": roof, "roofline_isolated": roof_iso, "valu": valu,
-            "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated"),
+            "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated", a.scene),
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
             "ms_finish_per_step": round(ms_fin / a.steps, 3),
             "extend_rays_per_step": round((segs - tail_segs) / a.steps), "paths_per_step": round(paths / a.steps),
             "tail_segments_per_step": round(tail_segs / a.steps),
+            "shade_hits_d0_per_step": round(sh_d0 / a.steps), "shade_hits_per_step": round(sh / a.steps),
+            "shade_survivors_per_step": round(sh_surv / a.steps),
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, nx, ny, a.seed, a.cpu_baseline_seconds)

@@ -193,7 +193,7 @@ struct RenderParams {
     uint32_t spp0;            // absolute sample index of the chunk's first sample
     uint32_t k0, k1;          // RNG key (seed)
     const uint32_t* pixlist;  // shard pixel q -> image pixel j
-    double* sb;               // sample colours [3][B] SoA, B = npix * chunk_spp
+    double* sb;               // sample colours [B][3] (one rgb record per work id), B = npix * chunk_spp
     uint32_t B;
 };
 

@@ -1008,11 +1008,16 @@ __device__ __forceinline__ void store_path(const PathState& st, uint32_t k, cons
     st.ray[k] = RayRec{p.o.x, p.o.y, p.o.z, p.d.x, p.d.y, p.d.z};
     st.path[k] = PathRec{p.T.x, p.T.y, p.T.z, p.wid, p.rng};
 }
+// a finished sample's colour: one 24-B record per work id (rgb together, so a
+// scattered sample write touches one 32-B sector instead of three lines)
+__device__ __forceinline__ void put_sample(const RenderParams& rp, const uint32_t w, const double r, const double g,
+                                           const double b) {
+    double* o = rp.sb + 3u * (size_t)w;
+    o[0] = r; o[1] = g; o[2] = b;
+}
 // path done: sample colour = T (*) L into the chunk's sample buffer
 __device__ __forceinline__ void write_sample(const RenderParams& rp, const PathRegs& p, const v3 L) {
-    rp.sb[p.wid] = p.T.x * L.x;
-    rp.sb[rp.B + p.wid] = p.T.y * L.y;
-    rp.sb[2u * rp.B + p.wid] = p.T.z * L.z;
+    put_sample(rp, p.wid, p.T.x * L.x, p.T.y * L.y, p.T.z * L.z);
 }
 __device__ __forceinline__ v3 sky_radiance(const DevScene& sc, const v3 d) {
     if (sc.sky != 0) return mk(0.0, 0.0, 0.0);            // black main.scm:97-98
@@ -1117,14 +1122,10 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         if (leaf < 0) {
             const v3 L = sky_radiance(sc, d);
             if (depth0) {                                // throughput 1: (* 1 x) = x
-                rp.sb[i] = 1.0 * L.x;
-                rp.sb[rp.B + i] = 1.0 * L.y;
-                rp.sb[2u * rp.B + i] = 1.0 * L.z;
+                put_sample(rp, i, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
             } else {
                 const PathRec P = st.path[i];
-                rp.sb[P.wid] = P.tr * L.x;
-                rp.sb[rp.B + P.wid] = P.tg * L.y;
-                rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
+                put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
             }
         } else {
             hit.h[i] = HitRec{t, leaf, 0};
@@ -1213,14 +1214,10 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
             if (best < 0) {
                 const v3 L = sky_radiance(sc, d);
                 if (depth0) {                                // throughput 1: (* 1 x) = x
-                    rp.sb[i] = 1.0 * L.x;
-                    rp.sb[rp.B + i] = 1.0 * L.y;
-                    rp.sb[2u * rp.B + i] = 1.0 * L.z;
+                    put_sample(rp, i, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
                 } else {
                     const PathRec P = st.path[i];
-                    rp.sb[P.wid] = P.tr * L.x;
-                    rp.sb[rp.B + P.wid] = P.tg * L.y;
-                    rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
+                    put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
                 }
             } else {
                 hit.h[i] = HitRec{closest, best, 0};
@@ -1441,9 +1438,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);
                 const PathRec P = st.path[i];
-                rp.sb[P.wid] = P.tr * L.x;
-                rp.sb[rp.B + P.wid] = P.tg * L.y;
-                rp.sb[2u * rp.B + P.wid] = P.tb * L.z;
+                put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
             } else {
                 hit.h[i] = HitRec{t, leaf, 0};
                 cls = s_cls[leaf];
@@ -1509,9 +1504,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const 
                                                 t0, ta);
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);            // throughput 1: (* 1 x) = x
-                rp.sb[w] = 1.0 * L.x;
-                rp.sb[rp.B + w] = 1.0 * L.y;
-                rp.sb[2u * rp.B + w] = 1.0 * L.z;
+                put_sample(rp, w, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
             } else {
                 st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};   // depth-0 state for the shade kernels
                 st.tm[w] = time;
@@ -1995,13 +1988,12 @@ __global__ __launch_bounds__(256) void k_accumulate(const RenderParams rp, uint3
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= rp.npix) return;
     const uint32_t j = rp.pixlist[q];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        double acc = accum[3u * j + c];
-        const double* sbc = rp.sb + (size_t)c * rp.B;
-        for (uint32_t s = 0; s < S; ++s) acc = acc + sbc[(size_t)s * rp.npix + q];
-        accum[3u * j + c] = acc;
+    double a0 = accum[3u * j], a1 = accum[3u * j + 1], a2 = accum[3u * j + 2];
+    for (uint32_t s = 0; s < S; ++s) {                   // sample order per channel, as before
+        const double* r = rp.sb + 3u * ((size_t)s * rp.npix + q);
+        a0 = a0 + r[0]; a1 = a1 + r[1]; a2 = a2 + r[2];
     }
+    accum[3u * j] = a0; accum[3u * j + 1] = a1; accum[3u * j + 2] = a2;
 }
 
 // main.scm:481-491 — sqrt(sum/count), floor(255.99*min(1,c))

@@ -3,6 +3,7 @@
 #  1. rocprofv3 kernel trace + stats of bench.py at 256 spp
 #  2. PMC FETCH_SIZE, WRITE_SIZE and SQ f64 passes over k_extend (8 spp)
 #  3. profiles/pmc_extend.json from 2.
+#  4. PMC FETCH_SIZE, WRITE_SIZE over k_shade (8 spp) -> profiles/pmc_shade.json
 # usage: tools/profile_round.sh TAG
 set -e
 TAG=${1:-r01}
@@ -22,3 +23,11 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ
 python3 tools/pmc_to_json.py $O/fetch/f_counter_collection.csv $O/write/w_counter_collection.csv $O/fetch.log cover \
   profiles/pmc_extend.json $O/sq/s_counter_collection.csv
 cp profiles/pmc_extend.json $O/
+# 4. the same two byte counters over the shade kernels -> profiles/pmc_shade.json
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_shade -f csv -d $O/sfetch -o f -- \
+  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/sfetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_shade -f csv -d $O/swrite -o w -- \
+  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/swrite.log 2>&1
+python3 tools/pmc_shade_json.py $O/sfetch/f_counter_collection.csv $O/swrite/w_counter_collection.csv $O/sfetch.log cover \
+  profiles/pmc_shade.json
+cp profiles/pmc_shade.json $O/
