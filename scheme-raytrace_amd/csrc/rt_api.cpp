@@ -945,7 +945,7 @@ std::vector<uint32_t> make_pixlist(int nx, int ny, int shard, int nshard) {
 
 size_t max_paths() {
     const char* e = std::getenv("RTAMD_MAX_PATHS");
-    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)64 << 20;
+    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)96 << 20;
     return v < 1024 ? 1024 : v;
 }
 
@@ -1008,9 +1008,18 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     }
     const uint32_t npix = s->pix_n;
     if (npix == 0) return 0;
+    // Chunks of samples: as few as the pool cap allows, but at least four and
+    // an even count when the samples allow, so two render lanes end together
+    // (a frame of three chunks would leave one lane alone for a third of it).
     const size_t cap_paths = max_paths();
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
+    {
+        int n = (int)((spp_count + chunk - 1) / chunk);
+        if (n < 4) n = std::min(4, spp_count);
+        if (n > 1 && (n & 1) && n < spp_count) ++n;
+        chunk = (uint32_t)((spp_count + n - 1) / n);
+    }
     const int nchunks = (int)((spp_count + chunk - 1) / chunk);
     const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_wanted()), nchunks));
     const size_t cap = (size_t)npix * chunk;
