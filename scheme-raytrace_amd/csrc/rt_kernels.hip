@@ -1348,8 +1348,15 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
 #ifndef RT_EXTLDS_BLOCK
 #define RT_EXTLDS_BLOCK 512
 #endif
+// Waves per SIMD the LDS kernels are compiled for (VGPR cap 512 / waves).
+// k_extend_lds at 8 (64 VGPRs, spilling per-ray state outside the node loop)
+// measured +5 % on the overlapped two-lane frame against 6 (80 VGPRs), -1 %
+// with one lane; k_camera stays at 6 (8 made no difference and spills more).
 #ifndef RT_EXTLDS_WAVES
-#define RT_EXTLDS_WAVES 6
+#define RT_EXTLDS_WAVES 8
+#endif
+#ifndef RT_CAMERA_WAVES
+#define RT_CAMERA_WAVES 6
 #endif
 constexpr int kExtLdsBlock = RT_EXTLDS_BLOCK;
 // Copy n records of T from HBM into LDS, 16-B words, all threads of the block.
@@ -1458,7 +1465,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
 // something store their depth-0 state for the shade kernels.
 // =====================================================================
 template <bool ALL>
-__global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_camera(const DevScene sc, const RenderParams rp,
+__global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const DevScene sc, const RenderParams rp,
                                                                           const PathState st, const uint32_t n,
                                                                           HitBuf hit, uint32_t* __restrict__ queues,
                                                                           uint32_t qstride, uint32_t shard_cap,
