@@ -1,6 +1,6 @@
 #!/bin/bash
 # One round's profile set (run on the GPU box from the repo root):
-#  1. rocprofv3 kernel trace + stats of bench.py at 256 spp
+#  1. rocprofv3 kernel trace + stats of bench.py at 256 spp, and single-lane at the default 1024 spp
 #  2. PMC FETCH_SIZE, WRITE_SIZE and SQ f64 passes over k_extend (8 spp)
 #  3. profiles/pmc_extend.json from 2.
 #  4. PMC FETCH_SIZE, WRITE_SIZE over k_shade (8 spp) -> profiles/pmc_shade.json
@@ -13,6 +13,10 @@ O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- \
   python3 bench.py --spp 256 --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt.log 2>&1
+# the bench's own configuration (1024 spp) with one render lane: its per-launch
+# kernel durations are what roofline_isolated measures with HIP events
+RTAMD_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt_l1_full -o kt -- \
+  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt_l1_full.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_extend -f csv -d $O/fetch -o f -- \
   python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_extend -f csv -d $O/write -o w -- \
