@@ -1,6 +1,11 @@
 set -o pipefail
-O=gpurun_out/prof_r01k
+O=gpurun_out/ab16
 mkdir -p $O
 python -c "import torch, numpy" || exit 1
-RTAMD_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt_l1_full -o kt -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt_l1_full.log 2>&1 || exit 1
-grep "^{" $O/kt_l1_full.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline'])"
+B="timeout -k 10 100 python bench.py --no-cpu-baseline --no-isolated --spp 256 --steps 4"
+run() { tag=$1; shift; env "$@" > $O/$tag.log 2>&1 || { tail -5 $O/$tag.log; exit 1; }; python -c "import json; d=json.loads([l for l in open('$O/$tag.log').read().splitlines() if l.startswith('{')][-1]); print('$tag', d['value'], d['ms_per_step'])"; }
+L=scheme-raytrace_amd/rtamd
+run base $B
+run s5 RTAMD_LIB=$L/librtamd_s5.so $B
+run s6 RTAMD_LIB=$L/librtamd_s6.so $B
+run base2 $B
