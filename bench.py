@@ -9,12 +9,17 @@ integrator).  `value` = total segments / wall time over
 the timed steps (max over ranks), inputs resident in HBM.
 
 Multi-GPU (torch.distributed.run, one process per GPU): the frame is split
-into interleaved 16x16 tiles (tile t -> rank t % N, rt_render_device's
-shard arguments), each rank renders its tiles into a full-frame f64
-accumulator, and the per-rank accumulators are gathered onto rank 0 at frame
-end with one RCCL reduce over xGMI (tiles are disjoint, every other pixel is
-0.0, so the sum is the exact union).  Total work per step is fixed:
+into interleaved 16x16 tiles (tile t -> rank t % N); each rank renders its
+tiles into a compact accumulator of its own pixels (rt_render_shard_device)
+and rank 0 gathers the shards over RCCL / xGMI at frame end and scatters them
+into the frame (rtamd.dist.gather_frame; the pixels are disjoint, so the
+frame is bit-identical to one GPU's).  Total work per step is fixed:
 "scaling": "strong".
+
+Parity (the metric's "per-pixel RMS vs ref"): after the timed steps rank 0
+times the oracle on a 64-row band of the frame at the top sample indices
+(cpu_baseline) and renders the same band and passes on the GPU with the
+production schedule; rms_vs_oracle / max_abs / pixels_gt_1e-9 compare them.
 """
 import argparse
 import json
@@ -72,6 +77,17 @@ def shade_roofline(st, note, scene):
             "avg_launch_ms": round(st.ms_shade / st.extend_launches, 4), "note": note}
 
 
+def scene_device(info):
+    """rt_get_scene_info plus the LDS kernels' occupancy: resident blocks of
+    512 threads per CU -> waves per SIMD (4 SIMDs per CU)."""
+    out = dict(info)
+    cus = max(1, info["cus"])
+    for k in ("extend", "camera"):
+        blocks = info["%s_lds_blocks" % k]
+        out["%s_waves_per_simd" % k] = round(blocks / cus * 512 / 64 / 4, 2) if blocks else None
+    return out
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -83,38 +99,140 @@ def parse():
     p.add_argument("--scene", default="cover")
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
-    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true",
+                   help="skip the CPU baseline and with it the band parity check (both need the oracle)")
     p.add_argument("--no-profile-events", action="store_true")
     p.add_argument("--no-isolated", action="store_true", help="skip the single-lane profiling frame")
     return p.parse_args()
 
 
-def cpu_baseline(scene, nx, ny, seed, budget_s):
-    """Time the oracle (C f64 restatement, OpenMP over pixels) on a bounded
-    sample of the same workload: a 64-row band of the C2 frame, one spp per
-    call, repeated with successive sample indices until ~budget_s of work."""
+def host_cpu():
+    """The GPU box's host CPU as this process sees it: model, nproc, the
+    affinity set, the cgroup CPU quota and OMP_NUM_THREADS (the box gives a
+    one-GPU job a 16-CPU share of a much larger machine)."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["model"] = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "unknown")
+    except OSError:
+        info["model"] = "unknown"
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    share = info["affinity"] or 1
+    if quota:
+        share = min(share, max(1, int(quota)))
+    if info["omp_num_threads"] and info["omp_num_threads"].isdigit():
+        share = min(share, int(info["omp_num_threads"]))
+    info["threads_used"] = max(1, share)
+    return info
+
+
+def band_rows(ny):
+    rows = min(64, ny)
+    return max(0, ny // 3 - rows // 2), rows
+
+
+def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
+    """The oracle (C f64 restatement, OpenMP over pixels) timed on the host:
+    (1) on the process's whole CPU share, on a 64-row band of the frame at the
+        top sample indices (passes spp-P .. spp-1, P sized to ~budget_s); its
+        accumulator is also the parity reference for the GPU's band;
+    (2) on one thread, rows of the same band at pass spp-1 (~budget_s/3);
+    (3) config C1 (cover scene 200x100x8 spp) in full, all threads and one.
+    Returns (cpu_baseline dict, band reference)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle  # cpu_baseline leg only
-    threads = max(1, min(16, os.cpu_count() or 1))
+    from rtamd import scenes
+    host = host_cpu()
+    T = host["threads_used"]
     o = oracle.build_scene(scene)
-    acc = np.zeros(nx * ny * 3)
-    rows = min(64, ny)
-    y0 = max(0, ny // 3 - rows // 2)
+    y0, rows = band_rows(ny)
     lo, hi = y0 * nx, (y0 + rows) * nx
-    t_used, segs_total, passes = 0.0, 0, 0
-    while t_used < budget_s:
+    # calibrate: one pass over 8 rows
+    cal = np.zeros(nx * ny * 3)
+    t = time.perf_counter()
+    o.render(nx, ny, spp - 1, 1, seed, cal, lo, min(hi, lo + 8 * nx), T)
+    per_row_pass = (time.perf_counter() - t) / min(8, rows)
+    P = int(max(1, min(spp, budget_s / max(1e-9, per_row_pass * rows))))
+    acc = np.zeros(nx * ny * 3)
+    t = time.perf_counter()
+    _, segs = o.render(nx, ny, spp - P, P, seed, acc, lo, hi, T)
+    t_all = time.perf_counter() - t
+    # one thread: the band row by row, pass spp-1 then spp-2 ..., until ~budget/3
+    one = np.zeros(nx * ny * 3)
+    t1, segs1, done = 0.0, 0, 0
+    while t1 < budget_s / 3 and done < rows * spp:
+        r, k = done % rows, done // rows
         t = time.perf_counter()
-        _, segs = o.render(nx, ny, passes, 1, seed, acc, lo, hi, threads)
-        t_used += time.perf_counter() - t
-        segs_total += segs
-        passes += 1
-    rate = segs_total / t_used / 1e6
-    return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": "oracle/rt_oracle.c (C f64 restatement of the Scheme hot path, OpenMP, %d threads) on rows "
-                      "%d..%d of the %dx%d C2 frame, %d spp (%d segments, %.1f s); Gauche, the reference's "
-                      "runtime, is not installed on the box" % (threads, y0, y0 + rows, nx, ny, passes, segs_total,
-                                                                 t_used)}
+        _, sg = o.render(nx, ny, spp - 1 - k, 1, seed, one, lo + r * nx, lo + (r + 1) * nx, 1)
+        t1 += time.perf_counter() - t
+        segs1 += sg
+        done += 1
+    # C1 in full (SURVEY §8(d) d2: 200x100, 8 passes, seed 0x5EED0001)
+    c1 = oracle.build_scene(scenes.random_scene(200, 100))
+    c1_rates = {}
+    for th in (T, 1):
+        a = np.zeros(200 * 100 * 3)
+        t = time.perf_counter()
+        _, sg = c1.render(200, 100, 0, 8, 0x5EED0001, a, 0, -1, th)
+        c1_rates[th] = (sg / (time.perf_counter() - t) / 1e6, sg)
+    out = {"value": round(segs / t_all / 1e6, 3), "unit": "Mrays/s", "cores": T, "kind": "port",
+           "sample": "oracle/rt_oracle.c (C f64 restatement of the Scheme hot path, OpenMP, %d threads) on rows "
+                     "%d..%d of the %dx%d frame, passes %d..%d (%d segments, %.1f s); Gauche, the reference's "
+                     "runtime, is not installed on the box" % (T, y0, y0 + rows - 1, nx, ny, spp - P, spp - 1, segs,
+                                                                 t_all),
+           "single_thread": {"value": round(segs1 / t1 / 1e6, 4), "unit": "Mrays/s", "cores": 1,
+                             "sample": "%d row-passes of the band (rows %d..%d, passes from %d down; %d segments, "
+                                       "%.1f s)" % (done, y0, y0 + rows - 1, spp - 1, segs1, t1)},
+           "c1_full": {"config": "C1: cover scene 200x100x8 spp, seed 0x5EED0001, whole frame",
+                       "threads": {str(T): round(c1_rates[T][0], 3), "1": round(c1_rates[1][0], 4)},
+                       "unit": "Mrays/s", "segments": c1_rates[1][1]},
+           "host": host}
+    return out, {"acc": acc, "y0": y0, "rows": rows, "spp_begin": spp - P, "passes": P}
+
+
+def gpu_band_parity(scene, nx, ny, seed, ref, h, ctx):
+    """Render the cpu_baseline band (same rows, same top-of-frame passes) on
+    the GPU with the production schedule — rt_render_rows_device, the default
+    chunk policy (>= 4 chunks) and two render lanes, so k_camera, k_extend_lds
+    and the k_shade kernels do the work — and compare with the oracle's
+    accumulator.  Parity metric: per-pixel linear-RGB RMS of sum/passes."""
+    import numpy as np
+    import torch
+    from rtamd import gpu
+    acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    gpu.render_rows_device(scene, nx, ny, ref["y0"], ref["rows"], ref["spp_begin"], ref["passes"], seed,
+                           acc.data_ptr(), ctx=ctx)
+    st = gpu.stats(h)
+    torch.cuda.synchronize()
+    lo, hi = 3 * ref["y0"] * nx, 3 * (ref["y0"] + ref["rows"]) * nx
+    P = ref["passes"]
+    got = acc.cpu().numpy()[lo:hi] / P
+    exp = ref["acc"][lo:hi] / P
+    d = np.abs(got - exp)
+    rms = float(np.sqrt(np.mean(d ** 2)))
+    return {"rms_vs_oracle": rms, "max_abs": float(d.max()),
+            "pixels_gt_1e-9": int((d.reshape(-1, 3).max(axis=1) > 1e-9).sum()),
+            "pixels": int(d.size // 3), "tolerance_rms": 1e-4, "pass": bool(rms <= 1e-4),
+            "rows": "%d..%d" % (ref["y0"], ref["y0"] + ref["rows"] - 1),
+            "passes": "%d..%d" % (ref["spp_begin"], ref["spp_begin"] + P - 1),
+            "gpu_schedule": {"chunks": int(st.chunks), "lanes": int(st.lanes), "paths": int(st.paths),
+                             "wavefront_segments": int(st.extend_rays), "tail_paths": int(st.finish_paths)},
+            "note": "oracle = oracle/rt_oracle.c on the host, GPU = rt_render_rows_device (production schedule)"}
 
 
 SCENE_CONFIG = {"cover": "C2", "cover_marble": "C3", "cornell": "C4", "cornell_mixture": "C4-mixture", "curves": "C5"}
@@ -137,6 +255,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from rtamd import dist as rdist
     from rtamd import gpu, scenes
     from rtamd._lib import call
 
@@ -148,18 +267,16 @@ def main():
     ctx = gpu.default_context(local)
     h = gpu.upload(scene, ctx)                      # one-time scene upload (not timed)
     call("rt_set_profiling", h, 0 if a.no_profile_events else 1)
-    accum = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
-    lib_stream = None                               # librtamd's own stream (events live there)
+    # world == 1: the frame accumulator; world > 1: this rank's compact shard (its tiles only), gathered
+    # onto rank 0 over RCCL at frame end (rtamd.dist.gather_frame)
+    frame = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda") if world == 1 else None
+    local = torch.zeros(rdist.local_size(nx, ny, rank, world), dtype=torch.float64, device="cuda") \
+        if world > 1 else None
 
     def step():
-        accum.zero_()
-        torch.cuda.synchronize()
-        gpu.render_device(scene, nx, ny, 0, spp, a.seed, accum.data_ptr(), shard=rank, nshard=world,
-                          stream=lib_stream, ctx=ctx)
-        s = gpu.stats(h)
-        if world > 1:
-            dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)   # RCCL gather of disjoint tiles
-        return s
+        (frame if world == 1 else local).zero_()
+        rdist.render_frame(scene, nx, ny, 0, spp, a.seed, rank, world, local=local, frame=frame, ctx=ctx)
+        return gpu.stats(h)
 
     for _ in range(a.warmup):
         step()
@@ -259,6 +376,7 @@ def main():
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
             "roofline": roof, "roofline_isolated": roof_iso, "valu": valu,
             "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated", a.scene),
+            "scene_device": scene_device(gpu.scene_info(h)),
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
@@ -268,10 +386,14 @@ def main():
             "shade_hits_d0_per_step": round(sh_d0 / a.steps), "shade_hits_per_step": round(sh / a.steps),
             "shade_survivors_per_step": round(sh_surv / a.steps),
         }
+        out["cpu_baseline"] = None
+        out["parity"] = None
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(scene, nx, ny, a.seed, a.cpu_baseline_seconds)
-        else:
-            out["cpu_baseline"] = None
+            out["cpu_baseline"], ref = cpu_baseline(scene, nx, ny, spp, a.seed, a.cpu_baseline_seconds)
+            par = gpu_band_parity(scene, nx, ny, a.seed, ref, h, ctx)
+            out["parity"] = par
+            for k in ("rms_vs_oracle", "max_abs", "pixels_gt_1e-9"):
+                out[k] = par[k]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -142,11 +142,42 @@ int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t 
 int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
                      int shard_index, int shard_count, double* accum_device, void* stream);
 
+/* Rows [y_begin, y_begin + y_count) only (same pass semantics as rt_render): the
+ * band of the frame trace-line (main.scm:452-469) renders one row of.  accum is
+ * the whole nx*ny*3 frame; only the band's entries are read or written (the
+ * host version copies only the band across PCIe). */
+int rt_render_rows(int scene, int nx, int ny, int y_begin, int y_count, int spp_begin, int spp_count,
+                   uint64_t seed, double* accum_host);
+int rt_render_rows_device(int scene, int nx, int ny, int y_begin, int y_count, int spp_begin, int spp_count,
+                          uint64_t seed, double* accum_device, void* stream);
+/* trace-line (main.scm:452-469), as animate calls it (main.scm:533-544): add
+ * sample number `sample_count` (1-based) of every pixel of row y to raw_data
+ * (the *raw-data* running sum, nx*ny*3 doubles, y-up rows) and re-resolve row
+ * y of image (*image*, nx*ny*3 bytes) with sqrt(sum/sample_count).  Host
+ * buffers, caller-owned.  A frame done row by row equals the trace-all pass
+ * with the same sample_count bit for bit. */
+int rt_trace_line(int scene, int nx, int ny, int y, int sample_count, uint64_t seed, double* raw_data,
+                  uint8_t* image);
+/* One shard's tiles (as rt_render_device's shard arguments) into a COMPACT
+ * accumulator: accum_compact[3q..3q+2] is the running sum of pixel
+ * rt_shard_pixels(...)[q], so a rank holds and ships only its own pixels
+ * (multi-GPU gather, bench.py / rtamd.dist). */
+int rt_render_shard_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
+                           int shard_index, int shard_count, double* accum_compact, void* stream);
+
 /* The pixels shard `shard_index` of `shard_count` renders (host-only, no GPU
  * needed): interleaved 16x16 tiles in row-major tile order, tile t belongs to
  * shard t % shard_count; pixel j = y*nx + x, listed tile by tile.  Pass
  * out_pix = NULL to get the count only. */
 int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* out_pix, int64_t* out_count);
+
+/* Errors raised on the device.  Every loop of the kernels that waits on data
+ * (rejection samplers, curve subdivision walks, persistent kernels' per-path
+ * loops) has an iteration cap a valid random stream cannot reach, and queue
+ * appends never pass their shard's capacity: a kernel that would instead sets
+ * one of these bits and leaves the loop, and the render call fails with
+ * rt_last_error() naming them ("device fault (flags N): ..."). */
+enum { RT_FAULT_REJECT = 1, RT_FAULT_CURVE = 2, RT_FAULT_PATH = 4, RT_FAULT_SHARD = 8, RT_FAULT_LDS = 16 };
 
 /* Statistics of the last render on this scene. */
 typedef struct rt_stats {
@@ -164,8 +195,27 @@ typedef struct rt_stats {
     uint64_t shade_hits_d0;   /* camera-ray hits shaded by the wavefront shade kernels */
     uint64_t shade_hits;      /* deeper hits shaded by the wavefront shade kernels */
     uint64_t shade_survivors; /* paths the shade kernels wrote on to the next iteration */
+    uint32_t chunks;          /* sample chunks the render was cut into (path pools) */
+    uint32_t lanes;           /* render lanes (path pool + stream) kept in flight */
 } rt_stats;
 int rt_get_stats(int scene, rt_stats* out);
+
+/* What a committed scene became on the device (diagnostics for benchmarks
+ * and tests): primitive and tree sizes, and the LDS footprint and resident
+ * grid of the persistent LDS kernels (0 = the scene does not use them). */
+typedef struct rt_scene_info {
+    int32_t  leaves;          /* flattened primitives (leaf records) */
+    int32_t  groups;          /* closest-hit groups (a BVH counts as one) */
+    int32_t  bvh_nodes;       /* inner nodes of the all-times tree */
+    int32_t  bvh0_nodes;      /* inner nodes of the time-0 tree */
+    int32_t  tree_depth;      /* deepest tree level (the per-lane traversal stack) */
+    int32_t  bvh_solo;        /* 1: the world is exactly one BVH group */
+    uint32_t extend_lds_bytes, extend_lds_blocks;   /* k_extend_lds: LDS per block, resident blocks */
+    uint32_t camera_lds_bytes, camera_lds_blocks;   /* k_camera: the same */
+    int32_t  cus;             /* compute units of the context's device */
+    int32_t  reserved;
+} rt_scene_info;
+int rt_get_scene_info(int scene, rt_scene_info* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */
 int rt_set_profiling(int scene, int enabled);
 

@@ -30,7 +30,7 @@ hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, 
                          unsigned long long*, size_t, uint32_t, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
 size_t extend_lds_bytes(const DevScene&);
-hipError_t extend_lds_prepare(size_t, uint32_t*);
+hipError_t extend_lds_prepare(const DevScene&, size_t, uint32_t*);
 size_t camera_lds_bytes(const DevScene&);
 hipError_t camera_prepare(const DevScene&, size_t, uint32_t*);
 hipError_t launch_camera(const DevScene&, const RenderParams&, const PathState&, uint32_t, const HitBuf&, uint32_t*,
@@ -39,6 +39,7 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
                              const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, unsigned long long*,
                              hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
+hipError_t take_fault(uint32_t*);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -149,7 +150,7 @@ struct Scene {
     // render buffers: one path pool per lane (render_impl)
     DevBuf pixlist;
     std::unique_ptr<Lane> lanes[kLanes];
-    int pix_nx = -1, pix_ny = -1, pix_shard = -1, pix_nshard = -1;
+    int pix_nx = -1, pix_ny = -1, pix_y0 = -1, pix_y1 = -1, pix_shard = -1, pix_nshard = -1;
     uint32_t pix_n = 0;
     bool profiling = false;
     rt_stats stats{};
@@ -568,6 +569,7 @@ int commit_scene(Scene* s, int world) {
     std::vector<std::pair<int, int>> fsrc;           // (LEAF_SPHERE | LEAF_MSPHERE, local)
     int32_t fbvh2_root = 0;
     bool tree0_any_time = false;
+    bool tree0_direct = false;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
         // sphere trees: one primitive per leaf (measured fastest); curve trees keep 2
@@ -669,6 +671,21 @@ int commit_scene(Scene* s, int world) {
             }
             flatten_bvh2(b0.nodes, margin, [&](int b, int e) { return BvhLeaf{b, e - b, 0, 0, 0, 0, 0, 0}; },
                          fbvh2, fbleaf, fbvh2_root, lane_stack);
+            // Direct leaves: when every time-0 leaf holds exactly one sphere, put
+            // fsph (and its leaf-id map) in leaf order, so leaf k is sphere k and
+            // the SOLO LDS kernels need no leaf records (DevScene::bvh_solo).
+            tree0_direct = std::all_of(fbleaf.begin(), fbleaf.end(), [](const BvhLeaf& L) { return L.sn == 1; });
+            if (tree0_direct) {
+                std::vector<SphereRec> fs2(fbleaf.size());
+                std::vector<std::pair<int, int>> src2(fbleaf.size());
+                for (size_t k = 0; k < fbleaf.size(); ++k) {
+                    fs2[k] = fsph[(size_t)fbleaf[k].sb];
+                    src2[k] = fsrc[(size_t)fbleaf[k].sb];
+                    fbleaf[k].sb = (int32_t)k;
+                }
+                fsph.swap(fs2);
+                fsrc.swap(src2);
+            }
         }
     }
     std::vector<MediumRec> med;
@@ -865,6 +882,8 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_texs, s->texs, &d.texs)) return rc;
     d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();
     d.n_groups = (int)groups.size(); d.n_chains = (int)chains.size(); d.n_leaves = (int)leaves.size();
+    d.bvh_solo = (groups.size() == 1 && groups[0].type == GROUP_BVH && !bvh_has_bez && tree0_direct &&
+                  !std::getenv("RTAMD_NO_SOLO")) ? 1 : 0;
     d.n_mats = (int)s->mats.size(); d.n_texs = (int)s->texs.size();
     for (int k = 0; k < kLeafTypes; ++k) d.leaf_base[k] = base[k];
     d.has_perlin = s->have_perlin ? 1 : 0;
@@ -904,7 +923,7 @@ int commit_scene(Scene* s, int world) {
     if (!std::getenv("RTAMD_NO_EXTEND_LDS")) {
         const size_t lds = extend_lds_bytes(d);
         uint32_t mb = 0;
-        if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(lds, &mb) == hipSuccess && mb >= 256) {
+        if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
             s->ext_lds = lds;
             s->ext_lds_blocks = mb;
         }
@@ -928,19 +947,34 @@ int commit_scene(Scene* s, int world) {
 }
 
 // -------------------------------------------------------------- render
-// Interleaved 16x16 tiles (row-major tile order); tile t -> shard t % nshard.
-std::vector<uint32_t> make_pixlist(int nx, int ny, int shard, int nshard) {
+// The pixels a render covers: rows [y0, y1) of the frame (trace-all: every
+// row; trace-line, main.scm:452-469: one row), restricted to shard `shard` of
+// `nshard` interleaved 16x16 tiles (row-major tile order; tile t -> shard
+// t % nshard).  Listed tile by tile, pixel j = y*nx + x.
+struct PixSel { int y0, y1, shard, nshard; };
+PixSel full_frame(int ny) { return PixSel{0, ny, 0, 1}; }
+std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
     const int T = 16;
     const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
     std::vector<uint32_t> out;
-    out.reserve((size_t)nx * ny / nshard + T * T);
+    out.reserve((size_t)nx * (size_t)(ps.y1 - ps.y0) / (size_t)ps.nshard + T * T);
     for (int t = 0; t < tx * ty; ++t) {
-        if (t % nshard != shard) continue;
+        if (t % ps.nshard != ps.shard) continue;
         const int bx = (t % tx) * T, by = (t / tx) * T;
-        for (int yy = by; yy < std::min(by + T, ny); ++yy)
+        for (int yy = std::max(by, ps.y0); yy < std::min(std::min(by + T, ny), ps.y1); ++yy)
             for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
     }
     return out;
+}
+
+std::string fault_text(uint32_t f) {
+    std::string m = "device fault (flags " + std::to_string(f) + "):";
+    if (f & RT_FAULT_REJECT) m += " a rejection sampler exceeded its attempt cap;";
+    if (f & RT_FAULT_CURVE) m += " a curve walk exceeded its step bound;";
+    if (f & RT_FAULT_PATH) m += " a persistent kernel's path or ray exceeded its step bound;";
+    if (f & RT_FAULT_SHARD) m += " a queue shard overflowed (the append was dropped);";
+    if (f & RT_FAULT_LDS) m += " a persistent kernel's LDS allocation was too small;";
+    return m;
 }
 
 size_t max_paths() {
@@ -984,12 +1018,17 @@ PathState carve_state(void* base, size_t cap) {
     return st;
 }
 
-int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, int shard,
-                int nshard, double* accum, hipStream_t stream) {
+// Render passes spp_begin .. spp_begin+spp_count-1 of the pixels `ps` selects
+// into accum (indexed by image pixel j, or by the selection's own pixel index
+// q when `compact`).
+int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int spp_count, uint64_t seed,
+                double* accum, bool compact, hipStream_t stream) {
     if (!s->committed) return fail("scene not committed (rt_scene_commit)");
     if (nx <= 0 || ny <= 0) return fail("image size must be positive");
     if (spp_begin < 0 || spp_count < 0) return fail("spp_begin/spp_count must be >= 0");
-    if (nshard <= 0 || shard < 0 || shard >= nshard) return fail("invalid shard index/count");
+    if ((uint64_t)spp_begin + (uint64_t)spp_count > 0xFFFFFFFFull) return fail("sample index out of range");
+    if (ps.nshard <= 0 || ps.shard < 0 || ps.shard >= ps.nshard) return fail("invalid shard index/count");
+    if (ps.y0 < 0 || ps.y1 < ps.y0 || ps.y1 > ny) return fail("row range outside the image");
     if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
     Context* c = get_ctx(s->ctx);
     if (!c) return fail("scene's context was destroyed");
@@ -997,13 +1036,20 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     if (!stream) stream = c->stream;
     auto t_start = std::chrono::steady_clock::now();
     std::memset(&s->stats, 0, sizeof s->stats);
+    {
+        uint32_t stale = 0;
+        HIPCHK(take_fault(&stale));                  // a fault word left by another context's failed launch
+    }
     if (spp_count == 0) return 0;
 
-    if (s->pix_nx != nx || s->pix_ny != ny || s->pix_shard != shard || s->pix_nshard != nshard) {
-        std::vector<uint32_t> pl = make_pixlist(nx, ny, shard, nshard);
+    if (s->pix_nx != nx || s->pix_ny != ny || s->pix_y0 != ps.y0 || s->pix_y1 != ps.y1 || s->pix_shard != ps.shard ||
+        s->pix_nshard != ps.nshard) {
+        std::vector<uint32_t> pl = make_pixlist(nx, ny, ps);
+        s->pix_nx = -1;                              // stale until the upload below succeeds
         HIPCHK(s->pixlist.ensure(std::max<size_t>(1, pl.size()) * sizeof(uint32_t)));
         if (!pl.empty()) HIPCHK(hipMemcpy(s->pixlist.p, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        s->pix_nx = nx; s->pix_ny = ny; s->pix_shard = shard; s->pix_nshard = nshard;
+        s->pix_nx = nx; s->pix_ny = ny; s->pix_y0 = ps.y0; s->pix_y1 = ps.y1;
+        s->pix_shard = ps.shard; s->pix_nshard = ps.nshard;
         s->pix_n = (uint32_t)pl.size();
     }
     const uint32_t npix = s->pix_n;
@@ -1023,6 +1069,8 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
     const int nchunks = (int)((spp_count + chunk - 1) / chunk);
     const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_wanted()), nchunks));
     const size_t cap = (size_t)npix * chunk;
+    s->stats.chunks = (uint32_t)nchunks;
+    s->stats.lanes = (uint32_t)nlanes;
     // sharded compaction (rt_device.h kShards): shard capacity bounds what the
     // blocks of one shard can append in one wavefront step (extend: one item
     // per thread; the four shade kernels: grid-stride over at most 4096 blocks)
@@ -1059,6 +1107,18 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         L.state = Lane::IDLE;
         L.n_fin = 0;
     }
+    // An error return below leaves kernels queued on the lanes that may still
+    // write the caller's accumulator: drain every lane before returning.
+    struct Drain {
+        Scene* s; int n; bool armed = true;
+        ~Drain() {
+            if (!armed) return;
+            for (int i = 0; i < n; ++i)
+                if (s->lanes[i] && s->lanes[i]->stream) (void)hipStreamSynchronize(s->lanes[i]->stream);
+            uint32_t f = 0;
+            (void)take_fault(&f);                  // do not leak this render's fault bits into the next
+        }
+    } drain{s, nlanes};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const uint32_t qstride = (uint32_t)scap;
     const int mat_mask = s->dev.mat_mask;
@@ -1164,6 +1224,7 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         rp.pixlist = s->pixlist.as<const uint32_t>();
         rp.sb = L.sb.as<double>();
         rp.B = npix * L.S;
+        rp.compact = compact ? 1u : 0u;
         HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
         const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / tail_divisor());
         L.fused_camera = s->cam_lds != 0 && rp.B > tail;     // the tail kernel starts from raygen's state
@@ -1219,6 +1280,12 @@ int render_impl(Scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t
         HIPCHK(hipEventSynchronize(oldest->ev_cnt));
     }
     for (int li = 0; li < nlanes; ++li) HIPCHK(hipStreamSynchronize(s->lanes[li]->stream));
+    drain.armed = false;
+    {
+        uint32_t f = 0;
+        HIPCHK(take_fault(&f));
+        if (f) return fail(fault_text(f));
+    }
     for (int li = 0; li < nlanes; ++li) {
         Lane& L = *s->lanes[li];
         unsigned long long ctl[3] = {0, 0, 0};
@@ -1583,13 +1650,111 @@ int rt_get_stats(int scene, rt_stats* out) {
     return 0;
 }
 
+int rt_get_scene_info(int scene, rt_scene_info* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!out) return fail("null out pointer");
+    if (!s->committed) return fail("scene not committed (rt_scene_commit)");
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    const DevScene& d = s->dev;
+    std::memset(out, 0, sizeof *out);
+    out->leaves = d.n_leaves;
+    out->groups = d.n_groups;
+    out->bvh_nodes = d.n_bvh2;
+    out->bvh0_nodes = d.n_fbvh2;
+    out->tree_depth = d.lane_stack;
+    out->bvh_solo = d.bvh_solo;
+    out->extend_lds_bytes = (uint32_t)s->ext_lds;
+    out->extend_lds_blocks = s->ext_lds_blocks;
+    out->camera_lds_bytes = (uint32_t)s->cam_lds;
+    out->camera_lds_blocks = s->cam_blocks;
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    out->cus = cus;
+    return 0;
+}
+
 int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, int shard,
                      int nshard, double* accum, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
     Scene* s = get_scene(scene);
     if (!s) return fail("invalid scene handle");
     if (!accum) return fail("null accum");
-    return render_impl(s, nx, ny, spp_begin, spp_count, seed, shard, nshard, accum, (hipStream_t)stream);
+    if (ny <= 0) return fail("image size must be positive");
+    return render_impl(s, nx, ny, PixSel{0, ny, shard, nshard}, spp_begin, spp_count, seed, accum, false,
+                       (hipStream_t)stream);
+}
+
+int rt_render_shard_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, int shard,
+                           int nshard, double* accum_compact, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!accum_compact) return fail("null accum");
+    if (ny <= 0) return fail("image size must be positive");
+    return render_impl(s, nx, ny, PixSel{0, ny, shard, nshard}, spp_begin, spp_count, seed, accum_compact, true,
+                       (hipStream_t)stream);
+}
+
+int rt_render_rows_device(int scene, int nx, int ny, int y_begin, int y_count, int spp_begin, int spp_count,
+                          uint64_t seed, double* accum, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!accum) return fail("null accum");
+    if (y_begin < 0 || y_count < 0 || (int64_t)y_begin + y_count > ny) return fail("row range outside the image");
+    return render_impl(s, nx, ny, PixSel{y_begin, y_begin + y_count, 0, 1}, spp_begin, spp_count, seed, accum, false,
+                       (hipStream_t)stream);
+}
+
+namespace {
+// rows [y0, y0+yn) of a host accumulator through the context's device copy
+int render_rows_host(Scene* s, int nx, int ny, int y0, int yn, int spp_begin, int spp_count, uint64_t seed,
+                     double* accum_host) {
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if (y0 < 0 || yn < 0 || (int64_t)y0 + yn > ny) return fail("row range outside the image");
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(c->accum_tmp.ensure((size_t)nx * ny * 3 * sizeof(double)));
+    const size_t off = (size_t)y0 * nx * 3, cnt = (size_t)yn * nx * 3;
+    double* dev = c->accum_tmp.as<double>();
+    HIPCHK(hipMemcpyAsync(dev + off, accum_host + off, cnt * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (int rc = render_impl(s, nx, ny, PixSel{y0, y0 + yn, 0, 1}, spp_begin, spp_count, seed, dev, false, c->stream))
+        return rc;
+    HIPCHK(hipMemcpyAsync(accum_host + off, dev + off, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+}  // namespace
+
+int rt_render_rows(int scene, int nx, int ny, int y_begin, int y_count, int spp_begin, int spp_count, uint64_t seed,
+                   double* accum_host) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!accum_host) return fail("null accum");
+    return render_rows_host(s, nx, ny, y_begin, y_count, spp_begin, spp_count, seed, accum_host);
+}
+
+int rt_trace_line(int scene, int nx, int ny, int y, int sample_count, uint64_t seed, double* raw_data,
+                  uint8_t* image) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!raw_data || !image) return fail("null buffer");
+    if (sample_count < 1) return fail("sample_count is 1-based (main.scm:452)");
+    if (int rc = render_rows_host(s, nx, ny, y, 1, sample_count - 1, 1, seed, raw_data)) return rc;
+    // main.scm:462-469: correct-gamma of sum/sample-count, floor(255.99*min(1,c)), for row y only
+    const size_t b = (size_t)y * nx * 3, e = b + (size_t)nx * 3;
+    for (size_t i = b; i < e; ++i) {
+        const double c = std::sqrt(raw_data[i] / sample_count);
+        const double m = (1.0 < c) ? 1.0 : c;
+        image[i] = (uint8_t)std::floor(255.99 * m);
+    }
+    return 0;
 }
 
 int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed, double* accum_host) {
@@ -1604,7 +1769,8 @@ int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t 
     const size_t bytes = (size_t)nx * ny * 3 * sizeof(double);
     HIPCHK(c->accum_tmp.ensure(bytes));
     HIPCHK(hipMemcpyAsync(c->accum_tmp.p, accum_host, bytes, hipMemcpyHostToDevice, c->stream));
-    if (int rc = render_impl(s, nx, ny, spp_begin, spp_count, seed, 0, 1, c->accum_tmp.as<double>(), c->stream))
+    if (int rc = render_impl(s, nx, ny, full_frame(ny), spp_begin, spp_count, seed, c->accum_tmp.as<double>(), false,
+                             c->stream))
         return rc;
     HIPCHK(hipMemcpyAsync(accum_host, c->accum_tmp.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1615,7 +1781,7 @@ int rt_shard_pixels(int nx, int ny, int shard, int nshard, uint32_t* out_pix, in
     if (nx <= 0 || ny <= 0) return fail("image size must be positive");
     if (nshard <= 0 || shard < 0 || shard >= nshard) return fail("invalid shard index/count");
     if (!out_count) return fail("null out pointer");
-    const std::vector<uint32_t> pl = make_pixlist(nx, ny, shard, nshard);
+    const std::vector<uint32_t> pl = make_pixlist(nx, ny, PixSel{0, ny, shard, nshard});
     *out_count = (int64_t)pl.size();
     if (out_pix && !pl.empty()) std::memcpy(out_pix, pl.data(), pl.size() * sizeof(uint32_t));
     return 0;

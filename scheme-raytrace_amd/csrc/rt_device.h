@@ -11,6 +11,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/rt.h"
+
 namespace rtamd {
 
 constexpr int kMaxDepth = 100;                 // main.scm:26
@@ -18,6 +20,7 @@ constexpr double kTmin = 0.001;                // main.scm:104
 constexpr double kTmax = 999999999999.0;       // constant.scm:6
 constexpr double kPi = 3.141592653589793;      // math.const pi
 constexpr int kMaxChain = 4;                   // instance ops per leaf chain
+// device fault bits: RT_FAULT_* (include/rt.h); rt_kernels.hip g_fault, reported by render_impl
 
 enum TexType : int32_t { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_MARBLE = 3 };
 enum MatType : int32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
@@ -133,6 +136,9 @@ struct DevScene {
     int32_t n_fbvh2, n_fbleaf, n_fsph;
     int32_t tree0_any_time;                        // no moving spheres in the tree: the time-0 tree serves every ray
     int32_t n_bleaf;                               // leaves of the all-times tree
+    int32_t bvh_solo;                              // the world is exactly one BVH group (no other groups) and
+                                                   // every time-0 leaf is one sphere, fsph in leaf order: the
+                                                   // LDS kernels compile only the tree walk, with direct leaves
     const Chain* chains;   int32_t n_chains;
     const LeafInfo* leaves; int32_t n_leaves;
     const uint8_t* leaf_cls;                   // leaf id -> material type (a byte per leaf, padded to 16)
@@ -195,6 +201,7 @@ struct RenderParams {
     const uint32_t* pixlist;  // shard pixel q -> image pixel j
     double* sb;               // sample colours [B][3] (one rgb record per work id), B = npix * chunk_spp
     uint32_t B;
+    uint32_t compact;         // accumulator indexed by shard pixel q (rt_render_shard_device), not image pixel j
 };
 
 }  // namespace rtamd

@@ -33,6 +33,19 @@
 
 namespace rtamd {
 
+// --------------------------------------------------------------- faults
+// Device fault word (one per device).  Every loop that waits on data — the
+// rejection samplers, the curve subdivision walk, the persistent kernels'
+// per-path / per-ray loops — carries an iteration cap that a valid stream
+// cannot reach; a kernel that hits one, or would append past a queue shard,
+// sets a bit here and leaves the loop instead of hanging the device.
+// render_impl reads and clears the word after every render and fails the
+// call with rt_last_error naming the bits (rt_api.cpp fault_text).
+__device__ unsigned int g_fault;
+__device__ __forceinline__ void raise_fault(const unsigned int bit) { atomicOr(&g_fault, bit); }
+constexpr int kRejectCap = 4096;               // rejection sampler attempts (P(reject) <= 0.48 per attempt)
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;      // block_append / wave_append: the shard is full
+
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
                                          uint32_t k0, uint32_t k1) {
@@ -135,10 +148,11 @@ __device__ __forceinline__ void camera_ray(const DevScene& sc, const RenderParam
     // camera.scm:80-92
     const DevCamera& c = sc.cam;
     v3 p;
-    for (;;) {   // util.scm:17-23 random-in-unit-disk
+    for (int it = 0;; ++it) {   // util.scm:17-23 random-in-unit-disk
         const double a = g.next(), b = g.next();
         p = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, 0.0 * 2.0 - 0.0);
         if (dot(p, p) < 1.0) break;
+        if (it >= kRejectCap) { raise_fault(RT_FAULT_REJECT); p = mk(0.0, 0.0, 0.0); break; }
     }
     const v3 rd = p * c.lens;
     const v3 cu = mk(c.u[0], c.u[1], c.u[2]), cv = mk(c.v[0], c.v[1], c.v[2]);
@@ -310,7 +324,10 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
     int L = 0;
     uint32_t idx = 0;
     bool fresh = true;
-    for (;;) {
+    // the walk visits each of the <= 2^(leaf_level+1) subdivision nodes at most once
+    const uint32_t cap = 4u << leaf_level;
+    for (uint32_t it = 0;; ++it) {
+        if (it > cap) { raise_fault(RT_FAULT_CURVE); break; }
         if (!fresh) {
             c = root;
             for (int k = L - 1; k >= 0; --k) {
@@ -516,7 +533,10 @@ __device__ __forceinline__ int32_t stack_ref(const uint32_t e) { return (int32_t
 __device__ __forceinline__ int32_t stack_ref(const uint16_t e) { return (int32_t)(int16_t)e; }   // sign: leaf refs < 0
 // SE: stack entry type — uint32_t, or uint16_t (k_extend_lds / k_camera, trees
 // under 32768 nodes and leaves: child refs fit int16, halving the LDS stack).
-template <bool FROZEN, class SE = uint32_t>
+// DIRECT (FROZEN only, DevScene::bvh_solo): every time-0 leaf holds one
+// sphere and fsph is in leaf order, so leaf ref ~k tests fsph[k] directly
+// (no leaf record to fetch or keep in LDS).
+template <bool FROZEN, class SE = uint32_t, bool DIRECT = false>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, SE* lstk, const int lmax,
                                                  const BvhNode2* __restrict__ nodes,
@@ -572,34 +592,42 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
         }
         if (pend != kDone) {
-            const BvhLeaf L = leaves[~pend];
+            if constexpr (DIRECT) {
 #ifdef RT_STATS
-            ++n_leaf;
+                ++n_leaf; ++n_sph;
 #endif
-            if (FROZEN) {
-                for (int s = L.sb; s < L.sb + L.sn; ++s) {
-#ifdef RT_STATS
-                    ++n_sph;
-#endif
-                    const SphereRec S = fsph[s];
-                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, s, closest, fbest);
-                }
+                const SphereRec S = fsph[~pend];
+                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, ~pend, closest, fbest);
             } else {
-                for (int s = L.sb; s < L.sb + L.sn; ++s) {
+                const BvhLeaf L = leaves[~pend];
 #ifdef RT_STATS
-                    ++n_sph;
+                ++n_leaf;
 #endif
-                    const SphereRec S = sph[s];
-                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
-                }
-                for (int s = L.mb; s < L.mb + L.mn; ++s) {
+                if (FROZEN) {
+                    for (int s = L.sb; s < L.sb + L.sn; ++s) {
 #ifdef RT_STATS
-                    ++n_msph;
+                        ++n_sph;
 #endif
-                    const MSphereRec S = msph[s];
-                    const double frac = (time - S.t0) / S.den;
-                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                        const SphereRec S = fsph[s];
+                        sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, s, closest, fbest);
+                    }
+                } else {
+                    for (int s = L.sb; s < L.sb + L.sn; ++s) {
+#ifdef RT_STATS
+                        ++n_sph;
+#endif
+                        const SphereRec S = sph[s];
+                        sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                    }
+                    for (int s = L.mb; s < L.mb + L.mn; ++s) {
+#ifdef RT_STATS
+                        ++n_msph;
+#endif
+                        const MSphereRec S = msph[s];
+                        const double frac = (time - S.t0) / S.den;
+                        const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                        sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                    }
                 }
             }
             pend = kDone;
@@ -649,7 +677,10 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
 #ifdef RT_STATS
     uint32_t n_node = 0, n_leaf = 0, n_cand = 0, n_flush = 0, n_iter = 0;
 #endif
-    for (;;) {
+    // a lane visits each node and leaf at most once and queues each curve at most once, two per step
+    const uint32_t cap = 2u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf) + (uint32_t)sc.n_bez + 1024u;
+    for (uint32_t it = 0;; ++it) {          // wave-uniform
+        if (it > cap) { raise_fault(RT_FAULT_CURVE); break; }
 #ifdef RT_STATS
         ++n_iter;
 #endif
@@ -970,6 +1001,29 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
     return best;
 }
 
+// The LDS kernels' closest hit.  SOLO: the world is exactly one BVH group
+// (the cover scene: every object is a world-level sphere), so the kernel holds
+// only the tree walk — no code or registers for the other group types.
+// ALL_ONLY (k_camera over the all-times tree): a camera ray whose time is
+// +0.0 also walks the all-times tree, whose boxes bound every time and whose
+// moving-sphere test at time 0 computes the frozen centre with the same
+// operations — the same closest hit, so one walk is compiled instead of two.
+template <bool SOLO, bool ALL_ONLY = false>
+__device__ __forceinline__ int32_t closest_hit_lds(const DevScene& sc, const v3 o, const v3 d, const double time,
+                                                   double& closest, uint16_t* lstk, const int lmax, const Tree0 t0,
+                                                   const TreeA ta) {
+    if (!SOLO) return closest_hit<0, uint16_t>(sc, o, d, time, closest, lstk, lmax, nullptr, nullptr, t0, ta);
+    int32_t best = -1;
+    closest = kTmax;
+    if (!ALL_ONLY && (sc.tree0_any_time || __double_as_longlong(time) == 0ll))
+        bvh_closest_lane<true, uint16_t, true>(sc, o, d, time, closest, best, lstk, lmax, t0.nodes, nullptr, t0.sph,
+                                               nullptr, nullptr, t0.fid);
+    else
+        bvh_closest_lane<false, uint16_t>(sc, o, d, time, closest, best, lstk, lmax, ta.nodes, ta.leaves, nullptr,
+                                          ta.sph, ta.msph);
+    return best;
+}
+
 // ------------------------------------------------------------ path state
 struct PathRegs {
     v3 o, d;
@@ -1077,7 +1131,11 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
     }
     __syncthreads();
     uint32_t slot = 0;
-    if (cls >= 0) slot = shard * shard_cap + s_cnt[NC * 16 + cls] + s_cnt[cls * 16 + wave] + below;
+    if (cls >= 0) {
+        const uint32_t local = s_cnt[NC * 16 + cls] + s_cnt[cls * 16 + wave] + below;
+        if (local < shard_cap) slot = shard * shard_cap + local;
+        else { raise_fault(RT_FAULT_SHARD); slot = kNoSlot; }     // never write past the shard
+    }
     __syncthreads();                       // s_cnt is reused by the next call
     return slot;
 }
@@ -1133,7 +1191,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
         }
     }
     const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-    if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+    if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
 }
 
 // Wave-level append into the sharded material queues (block_append's layout:
@@ -1155,7 +1213,12 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
         uint32_t base = 0;
         if ((int)lane == leader) base = atomicAdd(counts + K * kCntStride, (uint32_t)__popcll(mk));
         base = (uint32_t)__shfl((int)base, leader, 64);
-        if (mine) { slot = (K % kShards) * shard_cap + base + lanes_below(mk); pending = false; }
+        if (mine) {
+            const uint32_t local = base + lanes_below(mk);
+            if (local < shard_cap) slot = (K % kShards) * shard_cap + local;
+            else { raise_fault(RT_FAULT_SHARD); slot = kNoSlot; }  // never write past the shard
+            pending = false;
+        }
         m = __ballot(pending);
     }
     return slot;
@@ -1196,10 +1259,15 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
     BvhNode2 N{};                                   // the lane's next node, loaded one iteration ahead
     int sp = 0, pb = 0, pe = 0;
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
+    // a ray takes at most one step per node / leaf and one queue step per two curves, and waits for
+    // batches that other lanes' steps trigger: bound its loop iterations (a valid walk stays far below)
+    const uint32_t ray_cap = 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
+    uint32_t ray_it = 0;
 #ifdef RT_STATS
     uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
 #endif
     for (;;) {
+        if (active && ++ray_it > ray_cap) { raise_fault(RT_FAULT_PATH); active = false; trav = false; pb = pe; }
 #ifdef RT_STATS
         ++st_iter;
         if (active && trav && pb >= pe) ++st_steps;
@@ -1226,7 +1294,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
             active = false;
         }
         const uint32_t slot = wave_append(cls, (k >> 8) & (uint32_t)(kShards - 1), counts, shard_cap);
-        if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
         // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
         const unsigned long long need = __ballot(!active);
         if (need && !exhausted) {
@@ -1257,6 +1325,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
                     sp = 0; node = sc.bvh2_root; trav = gb < sc.n_groups; pb = pe = 0;
                     if (trav && node >= 0) N = sc.bvh2[node];
                     active = true;
+                    ray_it = 0;
                 }
             }
         }
@@ -1376,8 +1445,10 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* src, const int n, con
 __host__ __device__ __forceinline__ size_t lds_tail_bytes(const DevScene& sc) {
     return ((size_t)sc.n_fsph * 4 + 15) / 16 * 16 + ((size_t)sc.n_leaves + 15) / 16 * 16;
 }
+// time-0 leaf records the LDS kernels stage: none for SOLO scenes (direct leaves)
+__host__ __device__ __forceinline__ int tree0_lds_leaves(const DevScene& sc) { return sc.bvh_solo ? 0 : sc.n_fbleaf; }
 __host__ __device__ __forceinline__ size_t extend_lds_need(const DevScene& sc) {
-    return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+    return (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)tree0_lds_leaves(sc) * sizeof(BvhLeaf) +
            (size_t)sc.n_fsph * sizeof(SphereRec) +
            (size_t)RT_EXTLDS_BLOCK * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint16_t) +
            lds_tail_bytes(sc);
@@ -1401,6 +1472,7 @@ __device__ __forceinline__ void stage_words(uint32_t* dst, const uint32_t* src, 
 // L1/L2 latency.  Sphere scenes only (no curves, media or Klein: F = 0).
 // =====================================================================
 
+template <bool SOLO>
 __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(const DevScene sc, const RenderParams rp,
                                                              const PathState st, const QView in, uint32_t n,
                                                              HitBuf hit, uint32_t* __restrict__ queues,
@@ -1409,9 +1481,9 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
                                                              unsigned long long* __restrict__ err) {
     extern __shared__ uint4 s_dyn[];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
-    const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
-    if (extend_lds_need(sc) > lds_bytes) {            // the carve below would leave the allocation
-        if (threadIdx.x == 0) atomicOr(err, 1ull);
+    const int nn = sc.n_fbvh2, nl = SOLO ? 0 : sc.n_fbleaf, ns = sc.n_fsph;
+    if (extend_lds_need(sc) > lds_bytes || (SOLO && !sc.bvh_solo)) {            // the carve below would leave the allocation
+        if (threadIdx.x == 0) { atomicOr(err, 1ull); raise_fault(RT_FAULT_LDS); }
         return;
     }
     BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_dyn);
@@ -1421,7 +1493,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
     int32_t* s_fid = reinterpret_cast<int32_t*>(s_lstack + (size_t)kExtLdsBlock * (sc.lane_stack > 0 ? sc.lane_stack : 1));
     uint8_t* s_cls = reinterpret_cast<uint8_t*>(s_fid) + ((size_t)ns * 4 + 15) / 16 * 16;
     stage_lds(s_nodes, sc.fbvh2, nn, kExtLdsBlock);      // the time-0 tree
-    stage_lds(s_leaves, sc.fbleaf, nl, kExtLdsBlock);
+    if (!SOLO) stage_lds(s_leaves, sc.fbleaf, nl, kExtLdsBlock);
     stage_lds(s_sph, sc.fsph, ns, kExtLdsBlock);
     stage_words(reinterpret_cast<uint32_t*>(s_fid), reinterpret_cast<const uint32_t*>(sc.fid), ns, kExtLdsBlock);
     stage_words(reinterpret_cast<uint32_t*>(s_cls), reinterpret_cast<const uint32_t*>(sc.leaf_cls),
@@ -1440,8 +1512,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
             const v3 o = mk(R.ox, R.oy, R.oz);
             const v3 d = mk(R.dx, R.dy, R.dz);
             double t;
-            const int32_t leaf = closest_hit<0, uint16_t>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, nullptr, nullptr, t0,
-                                                treeA_hbm(sc));
+            const int32_t leaf = closest_hit_lds<SOLO>(sc, o, d, 0.0, t, s_lstack + threadIdx.x, LS, t0, treeA_hbm(sc));
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);
                 const PathRec P = st.path[i];
@@ -1452,7 +1523,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-        if (cls >= 0) queues[(size_t)cls * qstride + slot] = i;
+        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
     }
 }
 
@@ -1464,7 +1535,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
 // time-0 tree (no moving spheres: it serves every time).  Only rays that hit
 // something store their depth-0 state for the shade kernels.
 // =====================================================================
-template <bool ALL>
+template <bool ALL, bool SOLO>
 __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const DevScene sc, const RenderParams rp,
                                                                           const PathState st, const uint32_t n,
                                                                           HitBuf hit, uint32_t* __restrict__ queues,
@@ -1474,11 +1545,11 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
                                                                           unsigned long long* __restrict__ err) {
     extern __shared__ uint4 s_dyn[];
     __shared__ uint32_t s_cnt[4 * 16 + 4];
-    if ((ALL ? camera_lds_need(sc) : extend_lds_need(sc)) > lds_bytes) {
-        if (threadIdx.x == 0) atomicOr(err, 2ull);
+    if ((ALL ? camera_lds_need(sc) : extend_lds_need(sc)) > lds_bytes || (SOLO && !sc.bvh_solo)) {
+        if (threadIdx.x == 0) { atomicOr(err, 2ull); raise_fault(RT_FAULT_LDS); }
         return;
     }
-    const int nn = ALL ? sc.n_bvh2 : sc.n_fbvh2, nl = ALL ? sc.n_bleaf : sc.n_fbleaf;
+    const int nn = ALL ? sc.n_bvh2 : sc.n_fbvh2, nl = ALL ? sc.n_bleaf : (SOLO ? 0 : sc.n_fbleaf);
     const int ns = ALL ? sc.n_sph : sc.n_fsph, nm = ALL ? sc.n_msph : 0;
     BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_dyn);
     BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
@@ -1488,7 +1559,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
     int32_t* s_fid = reinterpret_cast<int32_t*>(s_lstack + (size_t)kExtLdsBlock * (sc.lane_stack > 0 ? sc.lane_stack : 1));
     uint8_t* s_cls = reinterpret_cast<uint8_t*>(s_fid) + ((size_t)sc.n_fsph * 4 + 15) / 16 * 16;
     stage_lds(s_nodes, ALL ? sc.bvh2 : sc.fbvh2, nn, kExtLdsBlock);
-    stage_lds(s_leaves, ALL ? sc.bleaf : sc.fbleaf, nl, kExtLdsBlock);
+    if (nl) stage_lds(s_leaves, ALL ? sc.bleaf : sc.fbleaf, nl, kExtLdsBlock);
     stage_lds(s_sph, ALL ? sc.sph : sc.fsph, ns, kExtLdsBlock);
     if (ALL) stage_lds(s_msph, sc.msph, nm, kExtLdsBlock);
     stage_words(reinterpret_cast<uint32_t*>(s_fid), reinterpret_cast<const uint32_t*>(sc.fid), sc.n_fsph, kExtLdsBlock);
@@ -1507,8 +1578,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
             Rng g;
             camera_ray(sc, rp, w, o, d, time, g);
             // ALL: a camera ray whose time is +0.0 (shutter t0 = t1 = 0) takes the time-0 tree from HBM
-            const int32_t leaf = closest_hit<0, uint16_t>(sc, o, d, time, t, s_lstack + threadIdx.x, LS, nullptr, nullptr,
-                                                t0, ta);
+            const int32_t leaf = closest_hit_lds<SOLO, ALL>(sc, o, d, time, t, s_lstack + threadIdx.x, LS, t0, ta);
             if (leaf < 0) {
                 const v3 L = sky_radiance(sc, d);            // throughput 1: (* 1 x) = x
                 put_sample(rp, w, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
@@ -1521,7 +1591,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-        if (cls >= 0) queues[(size_t)cls * qstride + slot] = w;
+        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = w;
     }
 }
 
@@ -1821,10 +1891,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     } else if (mt == MAT_METAL) {                            // material.scm:45-57 (R2)
         const v3 reflected = reflect(unit(rdir), nrm);
         v3 s;
-        for (;;) {                                           // util.scm:9-15
+        for (int it = 0;; ++it) {                            // util.scm:9-15
             const double a = g.next(), b = g.next(), c = g.next();
             s = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, c * 2.0 - 1.0);
             if (dot(s, s) < 1.0) break;
+            if (it >= kRejectCap) { raise_fault(RT_FAULT_REJECT); s = mk(0.0, 0.0, 0.0); break; }
         }
         const v3 sd = reflected + s * li.mparam;
         if (!(dot(sd, nrm) > 0.0)) return false;             // absorbed: emitted 0
@@ -1904,7 +1975,7 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
-        if (alive) store_path(out, slot, p);
+        if (alive && slot != kNoSlot) store_path(out, slot, p);
     }
 }
 
@@ -1949,7 +2020,7 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
     unsigned int* next = reinterpret_cast<unsigned int*>(tail_ctl + 1);
     const QMap qm = qmap(in);
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t segs = 0;
+    uint32_t segs = 0, pseg = 0;                    // pseg: segments of the lane's current path
     bool active = false, exhausted = false;
     PathRegs p;
     for (;;) {
@@ -1963,10 +2034,14 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             if (base + cnt >= n) exhausted = true;
             if (!active) {
                 const uint32_t k = base + lanes_below(need);
-                if (k < n) { load_path(st, qphys(qm, k), p, rp, depth); active = true; }
+                if (k < n) { load_path(st, qphys(qm, k), p, rp, depth); active = true; pseg = 0; }
             }
         }
         if (__ballot(active) == 0ull) break;
+        if (active && ++pseg > (uint32_t)kMaxDepth + 2u) {   // depth is capped at kMaxDepth (main.scm:26)
+            raise_fault(RT_FAULT_PATH);
+            active = false;
+        }
         if (active) {
             double t;
             ++segs;
@@ -1994,7 +2069,7 @@ __global__ __launch_bounds__(256) void k_accumulate(const RenderParams rp, uint3
                                                     double* __restrict__ accum) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= rp.npix) return;
-    const uint32_t j = rp.pixlist[q];
+    const uint32_t j = rp.compact ? q : rp.pixlist[q];
     double a0 = accum[3u * j], a1 = accum[3u * j + 1], a2 = accum[3u * j + 2];
     for (uint32_t s = 0; s < S; ++s) {                   // sample order per channel, as before
         const double* r = rp.sb + 3u * ((size_t)s * rp.npix + q);
@@ -2078,6 +2153,18 @@ size_t extend_lds_bytes(const DevScene& sc) {
     if (sc.n_fbvh2 >= 32768 || sc.n_fbleaf >= 32768) return 0;        // 16-bit stack entries
     return extend_lds_need(sc);
 }
+// the kernel instance a scene's LDS launches use (SOLO: the world is one BVH group)
+static const void* extend_lds_fn(const DevScene& sc) {
+    return sc.bvh_solo ? reinterpret_cast<const void*>(&k_extend_lds<true>)
+                       : reinterpret_cast<const void*>(&k_extend_lds<false>);
+}
+static const void* camera_fn(const DevScene& sc) {
+    if (sc.tree0_any_time)
+        return sc.bvh_solo ? reinterpret_cast<const void*>(&k_camera<false, true>)
+                           : reinterpret_cast<const void*>(&k_camera<false, false>);
+    return sc.bvh_solo ? reinterpret_cast<const void*>(&k_camera<true, true>)
+                       : reinterpret_cast<const void*>(&k_camera<true, false>);
+}
 hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
                              uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride,
                              uint32_t shard_cap, uint32_t* counts, uint32_t max_blocks, unsigned long long* err,
@@ -2086,20 +2173,26 @@ hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const P
     uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     blocks = (blocks + kShards - 1) / kShards * kShards;      // every shard gets the same number of blocks
-    hipLaunchKernelGGL(k_extend_lds, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit, queues,
-                       qstride, shard_cap, counts, (uint32_t)lds, err);
+    if (sc.bvh_solo)
+        hipLaunchKernelGGL(k_extend_lds<true>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit,
+                           queues, qstride, shard_cap, counts, (uint32_t)lds, err);
+    else
+        hipLaunchKernelGGL(k_extend_lds<false>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit,
+                           queues, qstride, shard_cap, counts, (uint32_t)lds, err);
     return hipGetLastError();
 }
-// grid of k_extend_lds: every block it can keep resident on the device at once
-hipError_t extend_lds_prepare(size_t lds, uint32_t* max_blocks) {
-    HIP_RETURN_IF(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_extend_lds),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+// resident blocks of a persistent LDS kernel: every block it can keep on the device at once
+static hipError_t resident_blocks(const void* f, size_t lds, uint32_t* max_blocks) {
+    HIP_RETURN_IF(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int dev = 0, cus = 0, per_cu = 0;
     HIP_RETURN_IF(hipGetDevice(&dev));
     HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_lds, kExtLdsBlock, lds));
+    HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kExtLdsBlock, lds));
     *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
     return hipSuccess;
+}
+hipError_t extend_lds_prepare(const DevScene& sc, size_t lds, uint32_t* max_blocks) {
+    return resident_blocks(extend_lds_fn(sc), lds, max_blocks);
 }
 // LDS bytes k_camera needs (0 = cannot run): the all-times tree when the scene
 // has moving spheres, else the time-0 tree
@@ -2110,18 +2203,7 @@ size_t camera_lds_bytes(const DevScene& sc) {
     return camera_lds_need(sc);
 }
 hipError_t camera_prepare(const DevScene& sc, size_t lds, uint32_t* max_blocks) {
-    const void* f = sc.tree0_any_time ? reinterpret_cast<const void*>(&k_camera<false>)
-                                      : reinterpret_cast<const void*>(&k_camera<true>);
-    HIP_RETURN_IF(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int dev = 0, cus = 0, per_cu = 0;
-    HIP_RETURN_IF(hipGetDevice(&dev));
-    HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (sc.tree0_any_time)
-        HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_camera<false>, kExtLdsBlock, lds));
-    else
-        HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_camera<true>, kExtLdsBlock, lds));
-    *max_blocks = (uint32_t)(cus * (per_cu > 0 ? per_cu : 0));
-    return hipSuccess;
+    return resident_blocks(camera_fn(sc), lds, max_blocks);
 }
 hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathState& st, uint32_t n,
                          const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap, uint32_t* counts,
@@ -2129,12 +2211,12 @@ hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathS
     uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     blocks = (blocks + kShards - 1) / kShards * kShards;
-    if (sc.tree0_any_time)
-        hipLaunchKernelGGL(k_camera<false>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,
-                           qstride, shard_cap, counts, (uint32_t)lds, err);
-    else
-        hipLaunchKernelGGL(k_camera<true>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,
-                           qstride, shard_cap, counts, (uint32_t)lds, err);
+#define RT_CAMERA(A, S)                                                                                       \
+    hipLaunchKernelGGL((k_camera<A, S>), dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,  \
+                       qstride, shard_cap, counts, (uint32_t)lds, err)
+    if (sc.tree0_any_time) { if (sc.bvh_solo) RT_CAMERA(false, true); else RT_CAMERA(false, false); }
+    else { if (sc.bvh_solo) RT_CAMERA(true, true); else RT_CAMERA(true, false); }
+#undef RT_CAMERA
     return hipGetLastError();
 }
 constexpr size_t kShadeLeafLds = 32768;      // stage the leaf records when they fit (256 leaves)
@@ -2211,6 +2293,17 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
 #undef RT_FINISH_F
 #undef RT_FINISH
     return hipGetLastError();
+}
+// the device fault word: read and clear (render_impl, after the render's streams are synchronised)
+hipError_t take_fault(uint32_t* out) {
+    uint32_t f = 0;
+    HIP_RETURN_IF(hipMemcpyFromSymbol(&f, HIP_SYMBOL(g_fault), sizeof f));
+    if (f) {
+        const uint32_t z = 0;
+        HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_fault), &z, sizeof z));
+    }
+    *out = f;
+    return hipSuccess;
 }
 #ifdef RT_STATS
 extern "C" int rt_debug_stats(unsigned long long* out, int reset) {

@@ -38,7 +38,17 @@ class RtStats(ctypes.Structure):
         ("shade_hits_d0", ctypes.c_uint64),
         ("shade_hits", ctypes.c_uint64),
         ("shade_survivors", ctypes.c_uint64),
+        ("chunks", ctypes.c_uint32),
+        ("lanes", ctypes.c_uint32),
     ]
+
+
+class RtSceneInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("leaves", "groups", "bvh_nodes", "bvh0_nodes", "tree_depth",
+                                              "bvh_solo")] + \
+               [(n, ctypes.c_uint32) for n in ("extend_lds_bytes", "extend_lds_blocks", "camera_lds_bytes",
+                                               "camera_lds_blocks")] + \
+               [("cus", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 # name -> argtypes (restype is always c_int status, except where noted)
@@ -85,8 +95,17 @@ _SIGNATURES = {
                   _c_double_p],
     "rt_render_device": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                          ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p],
+    "rt_render_rows": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_int, ctypes.c_uint64, _c_double_p],
+    "rt_render_rows_device": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p],
+    "rt_trace_line": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                      _c_double_p, _c_u8_p],
+    "rt_render_shard_device": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p],
     "rt_get_stats": [ctypes.c_int, ctypes.POINTER(RtStats)],
     "rt_set_profiling": [ctypes.c_int, ctypes.c_int],
+    "rt_get_scene_info": [ctypes.c_int, ctypes.POINTER(RtSceneInfo)],
     "rt_resolve_u8": [_c_double_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_u8_p],
     "rt_shard_pixels": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
                         ctypes.POINTER(ctypes.c_int64)],

@@ -1,0 +1,80 @@
+"""Multi-GPU frames: one process per GPU, tile-sharded.
+
+trace-all has no cross-pixel dependence (main.scm:471-491) and the counter RNG
+keys every sample by (seed, pixel, sample), so a frame splits into disjoint
+pixel sets with no exchange until the end.  Rank r renders the interleaved
+16x16 tiles t with t % world == r (rt_shard_pixels) into a COMPACT accumulator
+— its own pixels only, in shard order (rt_render_shard_device) — and rank 0
+gathers the shards over the process group (RCCL over xGMI with the "nccl"
+backend; gloo on the CPU) and scatters them into the y-up frame.  Each rank
+ships 1/world of the frame instead of a full-frame buffer, and the result is
+bit-identical to a one-process render (the pixels are disjoint, nothing is
+summed).
+
+``gather_frame`` is the exchange step; bench.py calls it through
+``render_frame`` on the GPU, tests/test_distributed.py calls it with gloo on
+CPU tensors.
+"""
+import numpy as np
+
+from . import gpu
+
+_pix_cache = {}
+
+
+def shard_pixels(nx, ny, world):
+    """Per-rank pixel lists (image pixel j = y*nx + x), rank r's in its compact order."""
+    key = (nx, ny, world)
+    if key not in _pix_cache:
+        _pix_cache[key] = [gpu.shard_pixels(nx, ny, r, world).astype(np.int64) for r in range(world)]
+    return _pix_cache[key]
+
+
+def gather_frame(local, nx, ny, rank, world, group=None):
+    """Gather every rank's compact accumulator (a 1-D float64 tensor of
+    3 x its pixel count) onto rank 0 and scatter it into an nx*ny*3 frame.
+    Returns the frame on rank 0 (on local's device), None on other ranks."""
+    import torch
+    import torch.distributed as dist
+
+    pix = shard_pixels(nx, ny, world)
+    counts = [len(p) for p in pix]
+    if local.numel() != 3 * counts[rank]:
+        raise ValueError("rank %d holds %d values, its shard has %d pixels" % (rank, local.numel(), counts[rank]))
+    width = 3 * max(counts)                     # collectives move equal-size buffers: pad to the largest shard
+    send = local
+    if local.numel() < width:
+        send = torch.zeros(width, dtype=local.dtype, device=local.device)
+        send[:local.numel()] = local
+    bufs = [torch.empty(width, dtype=local.dtype, device=local.device) for _ in range(world)] if rank == 0 else None
+    dist.gather(send, gather_list=bufs, dst=0, group=group)
+    if rank != 0:
+        return None
+    frame = torch.zeros(nx * ny * 3, dtype=local.dtype, device=local.device)
+    rows = frame.view(-1, 3)
+    for r in range(world):
+        idx = torch.from_numpy(pix[r]).to(local.device)
+        rows.index_copy_(0, idx, bufs[r][:3 * counts[r]].view(-1, 3))
+    return frame
+
+
+def render_frame(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local=None, frame=None, stream=None,
+                 ctx=None):
+    """One frame's passes on this rank's GPU.  world == 1: straight into `frame`
+    (a full-frame device tensor).  world > 1: this rank's tiles into `local`
+    (compact, 3 x shard pixels, zeroed by the caller), then gather_frame;
+    returns the frame on rank 0 and None elsewhere."""
+    if stream is None:                          # order after the caller's torch work (e.g. zeroing the buffers)
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    if world == 1:
+        gpu.render_device(scene, nx, ny, spp_begin, spp_count, seed, frame.data_ptr(), stream=stream, ctx=ctx)
+        return frame
+    gpu.render_shard_device(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local.data_ptr(), stream=stream,
+                            ctx=ctx)
+    return gather_frame(local, nx, ny, rank, world)
+
+
+def local_size(nx, ny, rank, world):
+    """Values in rank's compact accumulator (3 x its pixel count)."""
+    return 3 * len(shard_pixels(nx, ny, world)[rank])

@@ -159,6 +159,13 @@ def stats(scene_handle):
     return s
 
 
+def scene_info(scene_handle):
+    """rt_get_scene_info as a dict (tree sizes, LDS kernel footprints and grids)."""
+    s = _lib.RtSceneInfo()
+    call("rt_get_scene_info", scene_handle, ctypes.byref(s))
+    return {name: getattr(s, name) for name, _ in s._fields_ if name != "reserved"}
+
+
 def render_host(scene, nx, ny, spp_begin, spp_count, seed, accum, ctx=None):
     """rt_render: accum is a host float64 array of nx*ny*3 (updated in place)."""
     h = upload(scene, ctx)
@@ -177,6 +184,46 @@ def render_device(scene, nx, ny, spp_begin, spp_count, seed, accum_ptr, shard=0,
     """rt_render_device: accum_ptr is a device pointer (int) to nx*ny*3 doubles."""
     h = upload(scene, ctx)
     call("rt_render_device", h, nx, ny, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)), shard,
+         nshard, ctypes.c_void_p(accum_ptr), ctypes.c_void_p(stream or 0))
+    return h
+
+
+def render_rows_device(scene, nx, ny, y_begin, y_count, spp_begin, spp_count, seed, accum_ptr, stream=None,
+                       ctx=None):
+    """rt_render_rows_device: passes of rows [y_begin, y_begin+y_count) into a full-frame device accumulator."""
+    h = upload(scene, ctx)
+    call("rt_render_rows_device", h, nx, ny, y_begin, y_count, spp_begin, spp_count,
+         ctypes.c_uint64(seed & (2**64 - 1)), ctypes.c_void_p(accum_ptr), ctypes.c_void_p(stream or 0))
+    return h
+
+
+def render_rows_host(scene, nx, ny, y_begin, y_count, spp_begin, spp_count, seed, accum, ctx=None):
+    """rt_render_rows: as render_rows_device on a host float64 frame (only the band crosses PCIe)."""
+    h = upload(scene, ctx)
+    if accum.dtype != np.float64 or not accum.flags.c_contiguous or accum.size != nx * ny * 3:
+        raise ValueError("accum must be a contiguous float64 array of nx*ny*3 elements")
+    call("rt_render_rows", h, nx, ny, y_begin, y_count, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)),
+         accum.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return h
+
+
+def trace_line(scene, nx, ny, y, sample_count, seed, raw_data, image, ctx=None):
+    """rt_trace_line (main.scm:452-469): pass `sample_count` of row y into raw_data, row y of image resolved."""
+    h = upload(scene, ctx)
+    if raw_data.dtype != np.float64 or not raw_data.flags.c_contiguous or raw_data.size != nx * ny * 3:
+        raise ValueError("raw_data must be a contiguous float64 array of nx*ny*3 elements")
+    if image.dtype != np.uint8 or not image.flags.c_contiguous or image.size != nx * ny * 3:
+        raise ValueError("image must be a contiguous uint8 array of nx*ny*3 elements")
+    call("rt_trace_line", h, nx, ny, y, sample_count, ctypes.c_uint64(seed & (2**64 - 1)),
+         raw_data.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+         image.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return h
+
+
+def render_shard_device(scene, nx, ny, spp_begin, spp_count, seed, shard, nshard, accum_ptr, stream=None, ctx=None):
+    """rt_render_shard_device: one shard's tiles into a compact device accumulator (shard_pixels order)."""
+    h = upload(scene, ctx)
+    call("rt_render_shard_device", h, nx, ny, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)), shard,
          nshard, ctypes.c_void_p(accum_ptr), ctypes.c_void_p(stream or 0))
     return h
 

@@ -4,8 +4,11 @@
 (running f64 sum, nx*ny*3, y-up rows) and *image* (u8).  ``trace_all(scene,
 sample_count)`` is one pass exactly like the reference's: it adds sample
 number ``sample_count`` (1-based) to every pixel and re-resolves the image
-with sqrt(sum/sample_count).  ``render(scene, spp)`` runs many passes in one
-GPU call (same result as spp successive trace_all calls).
+with sqrt(sum/sample_count).  ``trace_line(scene, y, sample_count)`` is the
+reference's per-row pass (main.scm:452-469) and ``animate(scene)`` its GLUT
+display step (main.scm:533-544: one row per call, then the next pass).
+``render(scene, spp)`` runs many passes in one GPU call (same result as spp
+successive trace_all calls).
 """
 import numpy as np
 
@@ -22,6 +25,8 @@ class Renderer:
         self.raw_data = np.zeros(self.size_x * self.size_y * 3, dtype=np.float64)
         self.image = np.zeros(self.size_x * self.size_y * 3, dtype=np.uint8)
         self.sample_count = 0
+        self.current_y = 0            # *current-y* (main.scm:431)
+        self.anim_sample_count = 1    # *sample-count* (main.scm:531)
 
     def trace_all(self, scene, sample_count):
         """main.scm:471-491 — one sample per pixel (pass `sample_count`)."""
@@ -30,6 +35,29 @@ class Renderer:
         gpu.render_host(scene, self.size_x, self.size_y, sample_count - 1, 1, self.seed, self.raw_data, self.ctx)
         self.image = gpu.resolve_u8(self.raw_data, self.size_x, self.size_y, sample_count)
         self.sample_count = sample_count
+        return self.image
+
+    def trace_line(self, scene, y, sample_count):
+        """main.scm:452-469 — sample number `sample_count` (1-based) of row y only,
+        and row y of the image re-resolved; animate (main.scm:533-544) calls it
+        row by row, so a full sweep equals trace_all(scene, sample_count)."""
+        if sample_count < 1:
+            raise ValueError("sample-count is 1-based")
+        if not 0 <= y < self.size_y:
+            raise ValueError("row outside the image")
+        gpu.trace_line(scene, self.size_x, self.size_y, y, sample_count, self.seed, self.raw_data, self.image,
+                       self.ctx)
+        return self.image
+
+    def animate(self, scene):
+        """One display callback of main.scm:533-544 with *rendering?* on: trace
+        the current row; after the last row start the next sample pass."""
+        if self.current_y < self.size_y:
+            self.trace_line(scene, self.current_y, self.anim_sample_count)
+            self.current_y += 1
+        else:
+            self.anim_sample_count += 1
+            self.current_y = 0
         return self.image
 
     def render(self, scene, spp, spp_begin=None):

@@ -80,9 +80,23 @@ def test_full_width_band_parity(gpu_ctx, oracle_mod):
     assert np.isfinite(acc).all() and (acc.reshape(-1, 3).sum(axis=1) > 0).mean() > 0.99
 
 
-def test_accumulate_across_calls_bitwise(gpu_ctx):
+def _schedule(monkeypatch, schedule):
+    """"wavefront": the tail kernel off, so every depth runs through k_camera /
+    k_extend_lds / k_shade with sharded compaction (these small renders would
+    otherwise fit under the tail threshold and run in k_finish only)."""
+    if schedule == "wavefront":
+        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+
+
+SCHEDULES = ["tail", "wavefront"]
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_accumulate_across_calls_bitwise(gpu_ctx, monkeypatch, schedule):
     """spp passes in one call == the same passes split over calls (trace-all
     running sum, main.scm:480)."""
+    _schedule(monkeypatch, schedule)
     nx, ny = 40, 30
     scene = scenes.random_scene(nx, ny)
     a = np.zeros(nx * ny * 3)
@@ -93,8 +107,10 @@ def test_accumulate_across_calls_bitwise(gpu_ctx):
     assert np.array_equal(a, b)
 
 
-def test_batching_independent_bitwise(gpu_ctx, monkeypatch):
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_batching_independent_bitwise(gpu_ctx, monkeypatch, schedule):
     """Results do not depend on the path-pool size (chunking of samples)."""
+    _schedule(monkeypatch, schedule)
     nx, ny = 50, 20
     scene = scenes.cornell_box(nx, ny)
     a = np.zeros(nx * ny * 3)
@@ -105,11 +121,13 @@ def test_batching_independent_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("lanes", ["1", "2"])
-def test_lanes_and_chunks_bitwise(gpu_ctx, monkeypatch, lanes):
+def test_lanes_and_chunks_bitwise(gpu_ctx, monkeypatch, lanes, schedule):
     """Overlapped path pools (lanes) and many small chunks give the one-chunk
     image bit for bit: chunks are accumulated in sample order whichever lane
     finishes first."""
+    _schedule(monkeypatch, schedule)
     nx, ny, spp = 48, 40, 12
     scene = scenes.random_scene(nx, ny)
     a = np.zeros(nx * ny * 3)
@@ -121,9 +139,11 @@ def test_lanes_and_chunks_bitwise(gpu_ctx, monkeypatch, lanes):
     assert np.array_equal(a, b)
 
 
-def test_shards_union_bitwise(gpu_ctx):
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_shards_union_bitwise(gpu_ctx, monkeypatch, schedule):
     """Interleaved tile shards (the multi-GPU partition) reassemble the
     single-device image bit for bit."""
+    _schedule(monkeypatch, schedule)
     import torch
     nx, ny, spp = 70, 45, 3
     scene = scenes.random_scene(nx, ny)

@@ -1,0 +1,204 @@
+"""GPU tests of the production schedule and the row / shard entry points.
+
+The small parity renders in test_gpu_parity.py fit under the tail threshold
+(max(32768, B/128) paths, rt_api.cpp tail_threshold) and so run entirely in
+the tail kernel k_finish.  The tests here size the work so the wavefront
+kernels the benchmark times — k_camera, k_extend_lds, the per-material
+k_shade queues, sharded compaction, several sample chunks on two render
+lanes — do it, at high sample indices, and compare with the oracle (the C
+f64 restatement of the reference) or bitwise with other schedules.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from rtamd import gpu, scenes
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4
+SEED = 0x5EED0002
+
+
+def _wavefront_only(monkeypatch):
+    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+
+
+def _compare(a, b, n):
+    d = np.abs(a / n - b / n)
+    px = d.reshape(-1, 3).max(axis=1)
+    return float(np.sqrt(np.mean(d ** 2))), float(d.max()), int((px > 1e-9).sum()), px.size
+
+
+@pytest.fixture(scope="module")
+def c2_band(gpu_ctx, oracle_mod):
+    """Config C2 (cover scene, 1920x1080) rows 400..415, passes 1000..1023,
+    through the production schedule: 8 chunks of 3 passes (92 160 paths each,
+    above the tail threshold) on 2 lanes.  Returns the GPU accumulator, the
+    oracle's, and the render statistics."""
+    import torch
+    nx, ny, y0, rows, s0, n = 1920, 1080, 400, 16, 1000, 24
+    scene = scenes.random_scene(nx, ny)
+    old = {k: os.environ.get(k) for k in ("RTAMD_MAX_PATHS", "RTAMD_LANES")}
+    os.environ["RTAMD_MAX_PATHS"] = str(3 * rows * nx)
+    os.environ["RTAMD_LANES"] = "2"
+    try:
+        acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+        h = gpu.render_rows_device(scene, nx, ny, y0, rows, s0, n, SEED, acc.data_ptr())
+        st = gpu.stats(h)
+        got = acc.cpu().numpy()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ref = np.zeros(nx * ny * 3)
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    oracle_mod.build_scene(scene).render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=os.cpu_count() or 1)
+    return dict(nx=nx, ny=ny, y0=y0, rows=rows, s0=s0, n=n, scene=scene, got=got, ref=ref, stats=st, lo=lo, hi=hi)
+
+
+def test_production_band_vs_oracle(c2_band):
+    b = c2_band
+    st = b["stats"]
+    assert st.chunks >= 4 and st.lanes == 2, (st.chunks, st.lanes)
+    assert st.extend_rays > st.paths          # the wavefront kernels traced camera and scattered rays
+    lo, hi = b["lo"], b["hi"]
+    rms, dmax, nbad, npx = _compare(b["got"][3 * lo:3 * hi], b["ref"][3 * lo:3 * hi], b["n"])
+    print("C2 band rows %d..%d passes %d..%d: rms=%.3e max=%.3e pixels>1e-9: %d/%d chunks=%d lanes=%d"
+          % (b["y0"], b["y0"] + b["rows"] - 1, b["s0"], b["s0"] + b["n"] - 1, rms, dmax, nbad, npx, st.chunks,
+             st.lanes))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)
+    # nothing outside the band was touched
+    assert not b["got"][:3 * lo].any() and not b["got"][3 * hi:].any()
+
+
+def test_production_band_wavefront_to_depth_cap_bitwise(c2_band, monkeypatch):
+    """The same band with the tail kernel off (every depth in the wavefront,
+    one lane, other chunking): bit for bit the production result."""
+    import torch
+    b = c2_band
+    _wavefront_only(monkeypatch)
+    monkeypatch.setenv("RTAMD_LANES", "1")
+    monkeypatch.setenv("RTAMD_MAX_PATHS", str(5 * b["rows"] * b["nx"]))
+    acc = torch.zeros(b["nx"] * b["ny"] * 3, dtype=torch.float64, device="cuda")
+    h = gpu.render_rows_device(b["scene"], b["nx"], b["ny"], b["y0"], b["rows"], b["s0"], b["n"], SEED,
+                               acc.data_ptr())
+    assert gpu.stats(h).finish_paths == 0
+    assert np.array_equal(acc.cpu().numpy(), b["got"])
+
+
+def test_trace_line_row_by_row_equals_trace_all(gpu_ctx):
+    """trace-line (main.scm:452-469) over every row, pass by pass, and the
+    animate loop (main.scm:533-544) equal trace-all's passes bit for bit."""
+    from rtamd.render import Renderer
+    nx, ny = 48, 27
+    scene = scenes.random_scene(nx, ny)
+    a = Renderer(nx, ny, seed=SEED)
+    b = Renderer(nx, ny, seed=SEED)
+    c = Renderer(nx, ny, seed=SEED)
+    for k in (1, 2, 3):
+        img_a = a.trace_all(scene, k)
+        for y in range(ny):
+            img_b = b.trace_line(scene, y, k)
+        assert np.array_equal(a.raw_data, b.raw_data)
+        assert np.array_equal(img_a, img_b)
+    for _ in range(2 * (ny + 1)):            # two full sweeps of the GLUT loop
+        c.animate(scene)
+    d = Renderer(nx, ny, seed=SEED)
+    d.trace_all(scene, 1)
+    d.trace_all(scene, 2)
+    assert np.array_equal(c.raw_data, d.raw_data)
+    assert c.anim_sample_count == 3 and c.current_y == 0
+
+
+def test_rows_match_frame_bitwise(gpu_ctx, monkeypatch):
+    """Row bands (rt_render_rows) through the wavefront reassemble the
+    full-frame render bit for bit."""
+    _wavefront_only(monkeypatch)
+    nx, ny, spp = 64, 36, 4
+    scene = scenes.random_scene(nx, ny)
+    full = np.zeros(nx * ny * 3)
+    gpu.render_host(scene, nx, ny, 0, spp, SEED, full)
+    parts = np.zeros(nx * ny * 3)
+    for y0, yn in ((0, 7), (7, 20), (27, 9)):
+        gpu.render_rows_host(scene, nx, ny, y0, yn, 0, spp, SEED, parts)
+    assert np.array_equal(full, parts)
+
+
+def test_compact_shards_match_frame(gpu_ctx, monkeypatch):
+    """rt_render_shard_device (a rank's compact accumulator, as bench.py's
+    multi-GPU path uses) scattered by rt_shard_pixels equals the frame."""
+    import torch
+    from rtamd import dist as rdist
+    _wavefront_only(monkeypatch)
+    nx, ny, spp, world = 70, 45, 3, 3
+    scene = scenes.random_scene(nx, ny)
+    full = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    gpu.render_device(scene, nx, ny, 0, spp, SEED, full.data_ptr())
+    frame = torch.zeros_like(full)
+    for r in range(world):
+        local = torch.zeros(rdist.local_size(nx, ny, r, world), dtype=torch.float64, device="cuda")
+        gpu.render_shard_device(scene, nx, ny, 0, spp, SEED, r, world, local.data_ptr())
+        idx = torch.from_numpy(rdist.shard_pixels(nx, ny, world)[r]).cuda()
+        frame.view(-1, 3).index_copy_(0, idx, local.view(-1, 3))
+    torch.cuda.synchronize()
+    assert torch.equal(full, frame)
+
+
+def test_row_and_shard_errors(gpu_ctx):
+    import torch
+    from rtamd._lib import RtError
+    nx, ny = 16, 8
+    scene = scenes.random_scene(nx, ny)
+    acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    with pytest.raises(RtError):
+        gpu.render_rows_device(scene, nx, ny, 4, 5, 0, 1, SEED, acc.data_ptr())     # rows past the image
+    with pytest.raises(RtError):
+        gpu.render_rows_device(scene, nx, ny, -1, 2, 0, 1, SEED, acc.data_ptr())
+    with pytest.raises(ValueError):
+        gpu.trace_line(scene, nx, ny, 0, 1, SEED, np.zeros(nx * ny * 3), np.zeros(3, dtype=np.uint8))
+    from rtamd.render import Renderer
+    with pytest.raises(ValueError):
+        Renderer(nx, ny).trace_line(scene, ny, 1)
+    # the failed calls left nothing behind: a good render still works
+    gpu.render_rows_device(scene, nx, ny, 0, ny, 0, 1, SEED, acc.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.isfinite(acc).all() and acc.abs().sum() > 0
+
+
+def _noise_scene(nx, ny):
+    """t:noise-texture (texture.scm:25-28) on the ground and a sphere, a
+    marble sphere, a light: no reference scene uses noise-texture, so this
+    one exercises its GPU branch against the oracle."""
+    from rtamd import scene as g, vec as v
+    from rtamd.camera import make_camera
+    from rtamd import perlin
+    tables = perlin.from_seed(scenes.PERLIN_SEED)
+    objs = [g.make_sphere(v.vec3(0, -1000, 0), 1000, g.make_lambertian(g.noise_texture(4))),
+            g.make_sphere(v.vec3(0, 2, 0), 2, g.make_lambertian(g.noise_texture(0.7))),
+            g.make_sphere(v.vec3(4, 1.2, 1), 1.2, g.make_metal(g.noise_texture(2.5), 0.2)),
+            g.make_sphere(v.vec3(-4, 1.2, 0), 1.2, g.make_lambertian(g.marble_texture(1.5))),
+            g.make_xy_rect(3, 5, 1, 3, -2, g.make_diffuse_light(g.constant_texture(v.vec3(4, 4, 4))))]
+    cam = make_camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20, nx / ny, 0, 10, 0, 1)
+    return g.make_scene(objs, cam, g.sky_color, perlin=tables)
+
+
+@pytest.mark.parametrize("wavefront", [False, True])
+def test_noise_texture_vs_oracle(gpu_ctx, oracle_mod, monkeypatch, wavefront):
+    nx, ny, spp = 64, 36, 8
+    if wavefront:
+        _wavefront_only(monkeypatch)
+    sc = _noise_scene(nx, ny)
+    acc = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
+    ref, _ = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=os.cpu_count() or 1)
+    rms, dmax, nbad, npx = _compare(acc, ref, spp)
+    print("noise texture (wavefront=%s): rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (wavefront, rms, dmax, nbad, npx))
+    assert np.isfinite(acc).all() and acc.sum() > 0
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)

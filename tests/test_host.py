@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_errors_without_gpu():
     L = _lib.lib()
-    assert L.rt_abi_version() == 2
+    assert L.rt_abi_version() == 3
     h = ctypes.c_int(0)
     assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
     assert b"invalid context" in L.rt_last_error()
@@ -187,4 +187,24 @@ def test_c_example_builds_against_the_abi(tmp_path):
     import subprocess
     exe = _build_c_example(tmp_path)
     out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
-    assert out.strip() == "rt_abi_version 2"
+    assert out.strip() == "rt_abi_version 3"
+
+
+def test_load_points_and_points_to_bezier(tmp_path):
+    """load-points (points.scm:10-19): one "x,y,z" per line scaled by
+    magnitude, integers and decimals; points->bezier (points.scm:28-43): one
+    segment per interior pair, control points (p1, p1 + (p2-p0)/6, p2 -
+    (p3-p1)/6, p2)."""
+    from rtamd import points, vec as v
+    f = tmp_path / "pts.csv"
+    f.write_text("0,0,0\n1,2,3\n2.5,-1,0.5\n4,0,-2\n5,1,1\n")
+    pts = points.load_points(str(f), 10)
+    assert len(pts) == 5
+    assert tuple(pts[1]) == (10, 20, 30) and tuple(pts[2]) == (25.0, -10, 5.0)
+    bz = points.points_to_bezier(pts)
+    assert len(bz) == len(pts) - 3
+    p0, p1, p2, p3 = pts[0], pts[1], pts[2], pts[3]
+    want = [p1, v.sum(p1, v.scale(v.diff(p2, p0), 1 / 6)), v.diff(p2, v.scale(v.diff(p3, p1), 1 / 6)), p2]
+    for a, b in zip(bz[0], want):
+        assert tuple(a) == tuple(b)
+    assert tuple(bz[-1][0]) == tuple(pts[2]) and tuple(bz[-1][3]) == tuple(pts[3])
