@@ -327,7 +327,15 @@ def main():
         value = segs_all / elapsed / 1e6
         roof = None
         valu = None
+        valu_issue = None
         roof_iso = None
+        pm = None                       # PMC bytes / issue counters of the extend kernels (tools/profile_round.sh)
+        pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("scene") != a.scene or not pm.get("bytes_per_segment"):
+                pm = None
         if iso is not None and iso.extend_launches and iso.ms_extend > 0:
             bpl = extend_bytes(iso.extend_rays, iso.paths) / iso.extend_launches
             ams = iso.ms_extend / iso.extend_launches
@@ -336,6 +344,7 @@ def main():
                         "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": "k_extend + k_extend_lds",
                         "bytes_per_launch": round(bpl), "rays_per_launch": round(iso.extend_rays / iso.extend_launches),
                         "avg_launch_ms": round(ams, 4),
+                        "traffic": round(pm["bytes_per_segment"] * iso.extend_rays / iso.extend_launches) if pm else None,
                         "note": "one extra untimed frame with a single render lane (no concurrent kernels)"}
         if launches and ms_ext > 0:
             # wavefront extend launches only (the depth tail runs in k_finish)
@@ -345,13 +354,6 @@ def main():
             bytes_per_launch = extend_bytes(wf_segs, paths) / launches
             achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
             traffic = None
-            pm = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
-            if os.path.exists(pmc):
-                with open(pmc) as f:
-                    pm = json.load(f)
-                if pm.get("scene") != a.scene or not pm.get("bytes_per_segment"):
-                    pm = None
             if pm:
                 traffic = round(pm["bytes_per_segment"] * rays_per_launch)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -359,6 +361,18 @@ def main():
                     "kernel": "k_extend + k_extend_lds", "bytes_per_launch": round(bytes_per_launch),
                     "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4),
                     "note": "timed region; render lanes overlap, so launch durations include concurrent kernels"}
+            if pm and pm.get("valu_busy") is not None:
+                # share of SIMD cycles issuing VALU over the extend kernels (rocprofv3 VALUBusy, one bench frame):
+                # the issue-side roofline of these VALU / latency-bound kernels
+                valu_issue = {"bound": "valu_issue", "achieved": round(pm["valu_busy"] / 100.0, 4), "peak": 1.0,
+                              "unit": "fraction of SIMD cycles issuing VALU",
+                              "frac": round(pm["valu_busy"] / 100.0, 4),
+                              "lane_utilization": round(pm["valu_lane_utilization"] / 100.0, 4),
+                              "lds_busy": round(pm["lds_busy"] / 100.0, 4),
+                              "lds_bank_conflict_ratio": round(pm["lds_bank_conflict_ratio"], 4),
+                              "wait_share": round(pm["wait_share"], 4),
+                              "valu_instr_per_segment": round(pm["valu_instr_per_segment"], 2),
+                              "source": "profiles/pmc_extend.json (%s)" % pm.get("config", "")}
             if pm and pm.get("f64_flops_per_segment"):
                 tf = pm["f64_flops_per_segment"] * rays_per_launch / (avg_ms * 1e-3) / 1e12
                 valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
@@ -374,7 +388,7 @@ def main():
                                    % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp),
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": "tile-shard%d" % world if world > 1 else "single"},
-            "roofline": roof, "roofline_isolated": roof_iso, "valu": valu,
+            "roofline": roof, "roofline_isolated": roof_iso, "valu": valu, "valu_issue": valu_issue,
             "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated", a.scene),
             "scene_device": scene_device(gpu.scene_info(h)),
             "samples_per_s": round(paths_all / elapsed, 1),

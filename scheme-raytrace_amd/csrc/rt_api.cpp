@@ -22,10 +22,9 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, bool, unsigned int*, hipStream_t);
+                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
-                        const uint32_t*, const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t,
-                        hipStream_t);
+                        const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t, hipStream_t);
 hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
                          unsigned long long*, size_t, uint32_t, hipStream_t);
 hipError_t launch_accumulate(const RenderParams&, uint32_t, double*, hipStream_t);
@@ -33,11 +32,10 @@ size_t extend_lds_bytes(const DevScene&);
 hipError_t extend_lds_prepare(const DevScene&, size_t, uint32_t*);
 size_t camera_lds_bytes(const DevScene&);
 hipError_t camera_prepare(const DevScene&, size_t, uint32_t*);
-hipError_t launch_camera(const DevScene&, const RenderParams&, const PathState&, uint32_t, const HitBuf&, uint32_t*,
-                         uint32_t, uint32_t, uint32_t*, size_t, uint32_t, unsigned long long*, hipStream_t);
+hipError_t launch_camera(const DevScene&, const RenderParams&, const PathState&, uint32_t, const HitBuf&,
+                         uint32_t, uint32_t*, size_t, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
-                             const HitBuf&, uint32_t*, uint32_t, uint32_t, uint32_t*, uint32_t, unsigned long long*,
-                             hipStream_t);
+                             const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
 }  // namespace rtamd
@@ -98,7 +96,7 @@ struct Context {
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
 constexpr int kLanes = 4;                  // most lanes a render may use (RTAMD_LANES)
 struct Lane {
-    DevBuf st_a, st_b, hit, sb, counts, queues, seg_tail;
+    DevBuf st_a, st_b, hit, sb, counts, seg_tail;
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
     hipStream_t stream = nullptr;
     hipEvent_t ev_cnt = nullptr;               // the last iteration's survivor counts are on the host
@@ -289,6 +287,7 @@ struct BvhBuild {
     std::vector<PrimRef>& refs;
     std::vector<BvhNode> nodes;
     int leaf_max = 2;                 // RTAMD_BVH_LEAF
+    bool singles = false;             // split down to one primitive per leaf even where SAH would stop
     double trav_cost = 0.5;           // RTAMD_BVH_CT: node visit cost relative to one primitive test
     static constexpr int kBins = 16;
 
@@ -341,7 +340,7 @@ struct BvhBuild {
             }
             const double parent = area(lo, hi);
             const bool worth = best_k > 0 && (parent <= 0 || trav_cost + best / parent < (double)n);
-            if (!worth && n <= 2 * leaf_max) return make_leaf(node, b, e, lo, hi);
+            if (!worth && n <= 2 * leaf_max && !singles) return make_leaf(node, b, e, lo, hi);
             if (best_k > 0) {
                 auto it = std::partition(refs.begin() + b, refs.begin() + e,
                                          [&](const PrimRef& r) { return bin_of(r) < best_k; });
@@ -655,6 +654,7 @@ int commit_scene(Scene* s, int world) {
             BvhBuild b0{refs0, {}};
             b0.leaf_max = bb.leaf_max;
             b0.trav_cost = bb.trav_cost;
+            b0.singles = b0.leaf_max == 1;           // direct leaves (below) need one sphere per leaf
             b0.build(0, (int)refs0.size(), 0);
             // fsph in refs0 order; each entry remembers which sphere / moving sphere it is
             for (const PrimRef& r : refs0) {
@@ -1078,7 +1078,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     const size_t shard_cap = (cap + kShards - 1) / kShards + 4 * 32 * gmax + 256;
     const size_t scap = shard_cap * kShards;
     if (scap >= (1ull << 32)) return fail("path pool too large");
-    constexpr int kCountsPerIter = 5 * kShards * kCntStride;   // 4 material queues + survivors, 8 shards each
+    constexpr int kCountsPerIter = 5 * kShards * kCntStride;   // 4 material hit queues + survivors, 8 shards each
     constexpr int kIters = kMaxDepth + 4;
     // callers' prior work on `stream` (e.g. zeroing accum) comes first
     hipEvent_t ev_in = nullptr;
@@ -1094,10 +1094,9 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         if (s->profiling && !L.ev[0]) for (auto& e : L.ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(L.st_a.ensure(scap * kStateBytesPerPath));
         HIPCHK(L.st_b.ensure(scap * kStateBytesPerPath));
-        HIPCHK(L.hit.ensure(scap * sizeof(HitRec)));
+        HIPCHK(L.hit.ensure(4 * scap * sizeof(HitRec)));   // the 4 material hit queues (sharded like the survivors)
         HIPCHK(L.sb.ensure(cap * 3 * sizeof(double)));
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
-        HIPCHK(L.queues.ensure(scap * 4 * sizeof(uint32_t)));
         HIPCHK(L.seg_tail.ensure(3 * sizeof(unsigned long long)));   // tail segments, next tail path, errors
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
@@ -1120,8 +1119,6 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         }
     } drain{s, nlanes};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const uint32_t qstride = (uint32_t)scap;
-    const int mat_mask = s->dev.mat_mask;
     uint64_t seq = 0;
 
     // Enqueue the lane's next step for its current path count: one wavefront
@@ -1151,30 +1148,28 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             L.state = Lane::DONE;
             return 0;
         }
-        uint32_t* cnt = L.counts.as<uint32_t>() + L.depth * kCountsPerIter;   // [class][shard], survivors at 4
-        HitBuf hit{L.hit.as<HitRec>()};
-        uint32_t* queues = L.queues.as<uint32_t>();
+        uint32_t* cnt = L.counts.as<uint32_t>() + L.depth * kCountsPerIter;   // [material][shard], survivors at 4
+        HitBuf hit{L.hit.as<HitRec>(), (uint32_t)scap};
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[0], L.stream));
         if (L.depth == 0 && L.fused_camera)     // raygen + first closest hit in one kernel
-            HIPCHK(launch_camera(s->dev, L.rp, *L.cur, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
+            HIPCHK(launch_camera(s->dev, L.rp, *L.cur, L.n, hit, (uint32_t)shard_cap, cnt,
                                  s->cam_lds, s->cam_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
         else if (L.depth > 0 && s->ext_lds)     // every ray of a depth >= 1 launch has time +0.0
-            HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap,
+            HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, (uint32_t)shard_cap,
                                      cnt, s->ext_lds_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
         else
-            HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit, queues, qstride, (uint32_t)shard_cap, cnt,
-                                 L.depth == 0, reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1),
-                                 L.stream));
+            HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
+                                 (uint32_t)shard_cap, cnt, L.depth == 0,
+                                 reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1), L.stream));
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
         for (int mt = 0; mt < 4; ++mt) {
-            if (!(mat_mask & (1 << mt))) continue;
+            if (!(s->dev.mat_mask & (1 << mt))) continue;
             const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
-            HIPCHK(launch_shade(mt, s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, hit, queues + (size_t)mt * qstride, qv, L.n, *L.nxt, surv,
+            HIPCHK(launch_shade(mt, s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, hit, qv, L.n, *L.nxt, surv,
                                 (uint32_t)shard_cap, (uint32_t)L.depth, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[2], L.stream));
-        (void)surv;                                  // the whole row: queue counts (statistics) + survivors
         HIPCHK(hipMemcpyAsync(L.h_counts + L.depth * kCountsPerIter, cnt, kCountsPerIter * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, L.stream));
         HIPCHK(hipEventRecord(L.ev_cnt, L.stream));

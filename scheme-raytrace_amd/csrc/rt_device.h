@@ -174,8 +174,13 @@ struct PathState {
     double* tm;           // depth 0: time
     uint32_t* rng0;       // depth 0: draw counter
 };
-struct alignas(16) HitRec { double t; int32_t leaf, pad; };
-struct HitBuf { HitRec* h; };
+// The hit queues, one per material type: one record per ray that hit
+// something, appended by the closest-hit kernels in (block-)compaction order —
+// distance t, leaf id and the path's slot in the state pool — so a shade
+// kernel reads its queue front to back (no gather of a separate hit array).
+// Queue c starts at h + c * stride.
+struct alignas(16) HitRec { double t; int32_t leaf; uint32_t slot; };
+struct HitBuf { HitRec* h; uint32_t stride; };
 
 // Sharded queues.  Stream compaction appends through one atomic per block
 // and class on a counter chosen by blockIdx % kShards (8 XCDs), so no single

@@ -1148,7 +1148,6 @@ __device__ __forceinline__ uint32_t block_append(const int cls, uint32_t* __rest
 template <int F>
 __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderParams rp,
                                                 const PathState st, const QView in, uint32_t n, HitBuf hit,
-                                                uint32_t* __restrict__ queues, uint32_t qstride,
                                                 uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                 const bool depth0) {
     extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
@@ -1160,6 +1159,7 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     int cls = -1;
     uint32_t i = 0;
+    HitRec hr{};
     if (k < n) {
         i = qphys(qmap(in), k);
         const RayRec R = st.ray[i];
@@ -1186,12 +1186,12 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
                 put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
             }
         } else {
-            hit.h[i] = HitRec{t, leaf, 0};
+            hr = HitRec{t, leaf, i};
             cls = sc.leaves[leaf].mtype;
         }
     }
     const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-    if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
+    if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
 }
 
 // Wave-level append into the sharded material queues (block_append's layout:
@@ -1235,7 +1235,6 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // =====================================================================
 __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
-                                                       uint32_t* __restrict__ queues, uint32_t qstride,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                        const bool depth0, unsigned int* __restrict__ claim) {
     constexpr int F = kFeatCurves;
@@ -1277,6 +1276,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
         // 1. rays whose traversal ended and whose curves are all resolved: the
         //    groups after the BVH, then miss (sky) or hit + material queue
         int cls = -1;
+        HitRec hr{};
         if (active && !trav && pb >= pe && W.done[lane] == queued) {
             for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
             if (best < 0) {
@@ -1288,13 +1288,13 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
                     put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
                 }
             } else {
-                hit.h[i] = HitRec{closest, best, 0};
+                hr = HitRec{closest, best, i};
                 cls = sc.leaves[best].mtype;
             }
             active = false;
         }
         const uint32_t slot = wave_append(cls, (k >> 8) & (uint32_t)(kShards - 1), counts, shard_cap);
-        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
+        if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
         // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
         const unsigned long long need = __ballot(!active);
         if (need && !exhausted) {
@@ -1475,8 +1475,7 @@ __device__ __forceinline__ void stage_words(uint32_t* dst, const uint32_t* src, 
 template <bool SOLO>
 __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(const DevScene sc, const RenderParams rp,
                                                              const PathState st, const QView in, uint32_t n,
-                                                             HitBuf hit, uint32_t* __restrict__ queues,
-                                                             uint32_t qstride, uint32_t shard_cap,
+                                                             HitBuf hit, uint32_t shard_cap,
                                                              uint32_t* __restrict__ counts, const uint32_t lds_bytes,
                                                              unsigned long long* __restrict__ err) {
     extern __shared__ uint4 s_dyn[];
@@ -1505,9 +1504,9 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
     for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
         const uint32_t k = base + threadIdx.x;
         int cls = -1;
-        uint32_t i = 0;
+        HitRec hr{};
         if (k < n) {
-            i = qphys(qm, k);
+            const uint32_t i = qphys(qm, k);
             const RayRec R = st.ray[i];
             const v3 o = mk(R.ox, R.oy, R.oz);
             const v3 d = mk(R.dx, R.dy, R.dz);
@@ -1518,12 +1517,12 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
                 const PathRec P = st.path[i];
                 put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
             } else {
-                hit.h[i] = HitRec{t, leaf, 0};
+                hr = HitRec{t, leaf, i};
                 cls = s_cls[leaf];
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = i;
+        if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
     }
 }
 
@@ -1538,8 +1537,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
 template <bool ALL, bool SOLO>
 __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const DevScene sc, const RenderParams rp,
                                                                           const PathState st, const uint32_t n,
-                                                                          HitBuf hit, uint32_t* __restrict__ queues,
-                                                                          uint32_t qstride, uint32_t shard_cap,
+                                                                          HitBuf hit, uint32_t shard_cap,
                                                                           uint32_t* __restrict__ counts,
                                                                           const uint32_t lds_bytes,
                                                                           unsigned long long* __restrict__ err) {
@@ -1572,6 +1570,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
     for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
         const uint32_t w = base + threadIdx.x;
         int cls = -1;
+        HitRec hr{};
         if (w < n) {
             v3 o, d;
             double time, t;
@@ -1586,12 +1585,12 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
                 st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};   // depth-0 state for the shade kernels
                 st.tm[w] = time;
                 st.rng0[w] = g.ctr;
-                hit.h[w] = HitRec{t, leaf, 0};
+                hr = HitRec{t, leaf, w};
                 cls = s_cls[leaf];
             }
         }
         const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
-        if (cls >= 0 && slot != kNoSlot) queues[(size_t)cls * qstride + slot] = w;
+        if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
     }
 }
 
@@ -1939,16 +1938,21 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 }
 
 // =====================================================================
-// k_shade<MAT> — one material's queue; survivors compacted into `out`
+// k_shade<MAT> — one material's hit queue; survivors compacted into `out`.
+// (One kernel for all materials, sorting each block's hits by material in
+// LDS so the ray / path reads stay within one slot range, was measured and
+// not kept: its occupancy is the lambertian code's, and the memory-bound
+// metal / dielectric hits lost more than the shared lines saved — DESIGN §4.)
 // =====================================================================
-template <int MAT, bool PN, bool LS, bool LL>
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 1
 #endif
-__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp, const PathState in,
-                                               const HitBuf hit, const uint32_t* __restrict__ queue,
-                                               const QView qv, PathState out, uint32_t* __restrict__ out_counts,
-                                               uint32_t shard_cap, const uint32_t depth) {
+template <int MAT, bool PN, bool LS, bool LL>
+__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
+                                                                const PathState in, const HitRec* __restrict__ hq,
+                                                                const QView qv, PathState out,
+                                                                uint32_t* __restrict__ out_counts, uint32_t shard_cap,
+                                                                const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
@@ -1967,10 +1971,9 @@ __global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* _
         bool alive = false;
         PathRegs p;
         if (k < n) {
-            const uint32_t i = queue[qphys(qm, k)];
-            load_path(in, i, p, rp, depth);
+            const HitRec H = hq[qphys(qm, k)];
+            load_path(in, H.slot, p, rp, depth);
             v3 L;
-            const HitRec H = hit.h[i];
             alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
             if (!alive) write_sample(rp, p, L);
         }
@@ -2112,7 +2115,7 @@ static uint32_t curve_blocks() {            // cap on the persistent curve grid 
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
 }
 hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
-                         uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap,
+                         uint32_t n, const HitBuf& hit, uint32_t shard_cap,
                          uint32_t* counts, bool depth0, unsigned int* claim, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
@@ -2131,13 +2134,13 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
         uint32_t pb = blocks < occ_blocks ? blocks : occ_blocks;
         if (pb > curve_blocks()) pb = curve_blocks();
         HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-        hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), lds, s, sc, rp, st, in, n, hit, queues, qstride,
+        hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), lds, s, sc, rp, st, in, n, hit,
                            shard_cap, counts, depth0, claim);
         return hipGetLastError();
     }
 #define RT_EXTEND_F(F)                                                                                      \
-    hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit, queues,     \
-                       qstride, shard_cap, counts, depth0)
+    hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit,             \
+                       shard_cap, counts, depth0)
     switch (scene_features(sc)) {
     case 0: RT_EXTEND_F(0); break;
     case 1: RT_EXTEND_F(1); break;
@@ -2166,7 +2169,7 @@ static const void* camera_fn(const DevScene& sc) {
                        : reinterpret_cast<const void*>(&k_camera<true, false>);
 }
 hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
-                             uint32_t n, const HitBuf& hit, uint32_t* queues, uint32_t qstride,
+                             uint32_t n, const HitBuf& hit,
                              uint32_t shard_cap, uint32_t* counts, uint32_t max_blocks, unsigned long long* err,
                              hipStream_t s) {
     const size_t lds = extend_lds_bytes(sc);
@@ -2175,10 +2178,10 @@ hipError_t launch_extend_lds(const DevScene& sc, const RenderParams& rp, const P
     blocks = (blocks + kShards - 1) / kShards * kShards;      // every shard gets the same number of blocks
     if (sc.bvh_solo)
         hipLaunchKernelGGL(k_extend_lds<true>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit,
-                           queues, qstride, shard_cap, counts, (uint32_t)lds, err);
+                           shard_cap, counts, (uint32_t)lds, err);
     else
         hipLaunchKernelGGL(k_extend_lds<false>, dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, in, n, hit,
-                           queues, qstride, shard_cap, counts, (uint32_t)lds, err);
+                           shard_cap, counts, (uint32_t)lds, err);
     return hipGetLastError();
 }
 // resident blocks of a persistent LDS kernel: every block it can keep on the device at once
@@ -2206,14 +2209,14 @@ hipError_t camera_prepare(const DevScene& sc, size_t lds, uint32_t* max_blocks) 
     return resident_blocks(camera_fn(sc), lds, max_blocks);
 }
 hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathState& st, uint32_t n,
-                         const HitBuf& hit, uint32_t* queues, uint32_t qstride, uint32_t shard_cap, uint32_t* counts,
+                         const HitBuf& hit, uint32_t shard_cap, uint32_t* counts,
                          size_t lds, uint32_t max_blocks, unsigned long long* err, hipStream_t s) {
     uint32_t blocks = (n + kExtLdsBlock - 1) / kExtLdsBlock;
     if (blocks > max_blocks) blocks = max_blocks;
     blocks = (blocks + kShards - 1) / kShards * kShards;
 #define RT_CAMERA(A, S)                                                                                       \
-    hipLaunchKernelGGL((k_camera<A, S>), dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit, queues,  \
-                       qstride, shard_cap, counts, (uint32_t)lds, err)
+    hipLaunchKernelGGL((k_camera<A, S>), dim3(blocks), dim3(kExtLdsBlock), lds, s, sc, rp, st, n, hit,          \
+                       shard_cap, counts, (uint32_t)lds, err)
     if (sc.tree0_any_time) { if (sc.bvh_solo) RT_CAMERA(false, true); else RT_CAMERA(false, false); }
     else { if (sc.bvh_solo) RT_CAMERA(true, true); else RT_CAMERA(true, false); }
 #undef RT_CAMERA
@@ -2225,7 +2228,7 @@ static bool shade_leaves_hbm() {             // RTAMD_SHADE_LEAVES_HBM: keep the
     return v;
 }
 hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
-                        const HitBuf& hit, const uint32_t* queue, const QView& qv, uint32_t n_upper,
+                        const HitBuf& hit, const QView& qv, uint32_t n_upper,
                         const PathState& out, uint32_t* out_counts, uint32_t shard_cap, uint32_t depth, hipStream_t s) {
     // grid-stride cap: each block stages the leaf records once, so fewer,
     // longer-lived blocks (2048 measured best of 1024..8192: +1.5 % C2)
@@ -2238,14 +2241,15 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks == 0u) blocks = kShards;
+    const HitRec* hq = hit.h + (size_t)mat * hit.stride;
 #define RT_SHADE(M, PN, LS)                                                                                  \
     do {                                                                                                     \
         if (ll)                                                                                              \
-            hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hit,  \
-                               queue, qv, out, out_counts, shard_cap, depth);                                \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hq,   \
+                               qv, out, out_counts, shard_cap, depth);                                       \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hit,   \
-                               queue, qv, out, out_counts, shard_cap, depth);                                \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hq,    \
+                               qv, out, out_counts, shard_cap, depth);                                       \
     } while (0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture

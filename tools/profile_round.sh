@@ -1,37 +1,39 @@
 #!/bin/bash
-# One round's profile set (run on the GPU box from the repo root):
-#  1. rocprofv3 kernel trace + stats of bench.py at 256 spp, and single-lane at the default 1024 spp
-#  2. PMC FETCH_SIZE, WRITE_SIZE and SQ f64 passes over k_extend (8 spp)
-#  3. profiles/pmc_extend.json from 2.
-#  4. PMC FETCH_SIZE, WRITE_SIZE over k_shade (8 spp) -> profiles/pmc_shade.json
-# usage: tools/profile_round.sh TAG
+# One round's profile set at the BENCH configuration (C2: cover scene, 1920x1080x1024 spp, one frame),
+# run on the GPU box from the repo root:
+#   1. rocprofv3 kernel trace + stats, two render lanes (the timed bench) and one lane (roofline_isolated)
+#   2. PMC passes over every kernel of one frame (each pass a run of its own, within the per-block limits):
+#        fetch: FETCH_SIZE    write: WRITE_SIZE
+#        sq1:   VALUBusy VALUUtilization LdsUtil LdsBankConflict OccupancyPercent + SQ_WAIT_ANY SQ_INSTS_LDS
+#               SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES (+ GRBM_GUI_ACTIVE)
+#        sq2:   SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES + the f64 op counters + SQ_BUSY_CU_CYCLES
+#   3. tools/pmc_report.py -> profiles/pmc_round.json (per kernel family: bytes per item, VALU / LDS busy,
+#      lane utilisation, waits), and the extend / shade summaries bench.py reads (profiles/pmc_extend.json,
+#      profiles/pmc_shade.json)
+# usage: tools/profile_round.sh TAG [extra bench args]
 set -e
-TAG=${1:-r01}
+set -o pipefail
+TAG=${1:-r02}
+shift || true
 export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt -o kt -- \
-  python3 bench.py --spp 256 --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt.log 2>&1
-# the bench's own configuration (1024 spp) with one render lane: its per-launch
-# kernel durations are what roofline_isolated measures with HIP events
-RTAMD_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt_l1_full -o kt -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/kt_l1_full.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_extend -f csv -d $O/fetch -o f -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_extend -f csv -d $O/write -o w -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU \
-  --kernel-include-regex k_extend -f csv -d $O/sq -o s -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/sq.log 2>&1
-python3 tools/pmc_to_json.py $O/fetch/f_counter_collection.csv $O/write/w_counter_collection.csv $O/fetch.log cover \
-  profiles/pmc_extend.json $O/sq/s_counter_collection.csv
-cp profiles/pmc_extend.json $O/
-# 4. the same two byte counters over the shade kernels -> profiles/pmc_shade.json
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_shade -f csv -d $O/sfetch -o f -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/sfetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_shade -f csv -d $O/swrite -o w -- \
-  python3 bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-profile-events --no-isolated > $O/swrite.log 2>&1
-python3 tools/pmc_shade_json.py $O/sfetch/f_counter_collection.csv $O/swrite/w_counter_collection.csv $O/sfetch.log cover \
-  profiles/pmc_shade.json
-cp profiles/pmc_shade.json $O/
+B="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt2 -o kt -- $B > $O/kt2.log 2>&1
+echo "kt2 ok"
+RTAMD_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt1 -o kt -- $B > $O/kt1.log 2>&1
+echo "kt1 ok"
+P="$B --no-profile-events"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o f -- $P > $O/fetch.log 2>&1
+echo "fetch ok"
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o w -- $P > $O/write.log 2>&1
+echo "write ok"
+timeout -s KILL 300 rocprofv3 --pmc VALUBusy VALUUtilization LdsUtil LdsBankConflict OccupancyPercent SQ_WAIT_ANY \
+  SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/sq1 -o s -- $P > $O/sq1.log 2>&1
+echo "sq1 ok"
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
+  SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/sq2 -o s -- $P > $O/sq2.log 2>&1
+echo "sq2 ok"
+python3 tools/pmc_report.py $O $O/fetch.log profiles/pmc_round.json
+cp profiles/pmc_round.json profiles/pmc_extend.json profiles/pmc_shade.json $O/
