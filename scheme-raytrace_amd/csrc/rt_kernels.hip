@@ -1945,19 +1945,26 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 // metal / dielectric hits lost more than the shared lines saved — DESIGN §4.)
 // =====================================================================
 #ifndef RT_SHADE_WAVES
-#define RT_SHADE_WAVES 1
+#define RT_SHADE_WAVES 1               // lambertian / light: the compiler's choice (127 VGPRs, 4 waves)
 #endif
+#ifndef RT_SHADE_WAVES_MD
+#define RT_SHADE_WAVES_MD 1            // metal / dielectric (memory-bound gathers)
+#endif
+template <int MAT>
+constexpr int shade_waves() { return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD : RT_SHADE_WAVES; }
 template <int MAT, bool PN, bool LS, bool LL>
-__global__ __launch_bounds__(256, RT_SHADE_WAVES) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
+__global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
                                                                 const PathState in, const HitRec* __restrict__ hq,
                                                                 const QView qv, PathState out,
                                                                 uint32_t* __restrict__ out_counts, uint32_t shard_cap,
                                                                 const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
-    __shared__ PerlinLds P;
     __shared__ uint32_t s_cnt[16 + 1];
-    extern __shared__ uint4 s_leafdyn[];             // LL: the leaf records, staged once per block
+    // dynamic LDS: the leaf records (LL), then the Perlin tables (PN) — only
+    // what the scene uses, so the block's LDS does not cap the occupancy
+    extern __shared__ uint4 s_leafdyn[];
     LeafInfo* s_leaves = reinterpret_cast<LeafInfo*>(s_leafdyn);
+    PerlinLds& P = *reinterpret_cast<PerlinLds*>(s_leafdyn + (LL ? (size_t)sc.n_leaves * sizeof(LeafInfo) / 16 : 0));
     if (LL) stage_lds(s_leaves, sc.leaves, sc.n_leaves, 256);
     stage_perlin<PN>(sc, P);                         // (its barrier also covers the leaf staging)
     if (LL && !(PN && sc.has_perlin)) __syncthreads();
@@ -1993,19 +2000,22 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
                                                 const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
-    __shared__ PerlinLds P;
     // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
-    // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in k_extend_lds
+    // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in
+    // k_extend_lds, then, for scenes with Perlin tables, the tables
     extern __shared__ uint4 s_fdyn[];
     uint32_t* s_lstack = reinterpret_cast<uint32_t*>(s_fdyn);
     const int LS = sc.lane_stack;
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
+    const int words = (256 * (LS > 0 ? LS : 1) + 3) / 4;               // stack size in uint4
+    const size_t tree_words = tree0_lds ? ((size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+                                           (size_t)sc.n_fsph * sizeof(SphereRec)) / 16 : 0;
+    PerlinLds& P = *reinterpret_cast<PerlinLds*>(s_fdyn + words + tree_words);
     Tree0 t0 = tree0_hbm(sc);
     if (tree0_lds) {
         const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
-        const int words = (256 * (LS > 0 ? LS : 1) + 3) / 4;           // stack size in uint4
         BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_fdyn + words);
         BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
         SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
@@ -2248,13 +2258,15 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
             hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hq,   \
                                qv, out, out_counts, shard_cap, depth);                                       \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), 0, s, scd, rp, in, hq,    \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hq,  \
                                qv, out, out_counts, shard_cap, depth);                                       \
     } while (0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
-    const size_t lds = (size_t)sc.n_leaves * sizeof(LeafInfo);
-    const bool ll = lds <= kShadeLeafLds && !shade_leaves_hbm();
+    const size_t leaf_lds = (size_t)sc.n_leaves * sizeof(LeafInfo);
+    const bool ll = leaf_lds <= kShadeLeafLds && !shade_leaves_hbm();
+    // PN kernels of every material carry the Perlin tables (metal albedo may be a noise texture)
+    const size_t lds = (ll ? leaf_lds : 0) + ((pn && mat != MAT_DIELECTRIC && sc.has_perlin) ? sizeof(PerlinLds) : 0);
     switch (mat) {
     case MAT_LAMBERTIAN:
         if (ls) { if (pn) RT_SHADE(MAT_LAMBERTIAN, true, true); else RT_SHADE(MAT_LAMBERTIAN, false, true); }
@@ -2277,9 +2289,12 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
                         (size_t)sc.n_fsph * sizeof(SphereRec);
     const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
     if (tree0_lds) lds += tree;
+    // the Perlin tables ride at the end of the dynamic LDS, only where they are staged (PN and tables given)
+    const size_t perlin = sc.has_perlin ? sizeof(PerlinLds) : 0;
 #define RT_FINISH_F(F) RT_FINISH(F, true, true)
 #define RT_FINISH(F, PN, LS) \
-    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds, s, scd, rp, st, in, n, seg_count, tree0_lds, depth)
+    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, in, n, \
+                       seg_count, tree0_lds, depth)
     // the plain-sphere feature set also gets Perlin / light-mixture specialisations:
     // the tail kernel carries every material's code, so dropping the unused ones
     // trims its register file
