@@ -882,6 +882,14 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_texs, s->texs, &d.texs)) return rc;
     d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();
     d.n_groups = (int)groups.size(); d.n_chains = (int)chains.size(); d.n_leaves = (int)leaves.size();
+    d.msph_shared = 0;
+    if (!msph.empty() && !std::getenv("RTAMD_NO_MSPH_SHARED")) {
+        bool same = true;
+        for (const MSphereRec& m : msph)
+            same = same && std::memcmp(&m.t0, &msph[0].t0, sizeof(double)) == 0 &&
+                   std::memcmp(&m.den, &msph[0].den, sizeof(double)) == 0;
+        if (same) { d.msph_shared = 1; d.msph_t0 = msph[0].t0; d.msph_den = msph[0].den; }
+    }
     d.bvh_solo = (groups.size() == 1 && groups[0].type == GROUP_BVH && !bvh_has_bez && tree0_direct &&
                   !std::getenv("RTAMD_NO_SOLO")) ? 1 : 0;
     d.n_mats = (int)s->mats.size(); d.n_texs = (int)s->texs.size();

@@ -136,6 +136,8 @@ struct DevScene {
     int32_t n_fbvh2, n_fbleaf, n_fsph;
     int32_t tree0_any_time;                        // no moving spheres in the tree: the time-0 tree serves every ray
     int32_t n_bleaf;                               // leaves of the all-times tree
+    int32_t msph_shared;                           // every moving sphere has the same (t0, den = t1 - t0): the
+    double msph_t0, msph_den;                      // tree walk computes (time - t0) / den once per ray
     int32_t bvh_solo;                              // the world is exactly one BVH group (no other groups) and
                                                    // every time-0 leaf is one sphere, fsph in leaf order: the
                                                    // LDS kernels compile only the tree walk, with direct leaves

@@ -551,6 +551,9 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int32_t fbest = -1;                                       // FROZEN: fsph index of the best hit
+    // moving spheres sharing one shutter: center(time)'s (time - t0) / den is
+    // the same quotient for all of them, computed once (geometry.scm:181-184)
+    const double frac_shared = (!FROZEN && sc.msph_shared) ? (time - sc.msph_t0) / sc.msph_den : 0.0;
     int sp = 0;
     int32_t node = FROZEN ? sc.fbvh2_root : sc.bvh2_root, pend = kDone;
     float tcap = f32_up(closest);                              // box t range, updated after each leaf
@@ -624,7 +627,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                         ++n_msph;
 #endif
                         const MSphereRec S = msph[s];
-                        const double frac = (time - S.t0) / S.den;
+                        const double frac = sc.msph_shared ? frac_shared : (time - S.t0) / S.den;
                         const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                         sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
                     }
