@@ -182,17 +182,30 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
 // (tmin, closest) for spheres, non-strict for rects.  Every lane of a wave
 // walks the same group / primitive sequence, so the primitive records are
 // fetched once per wave through the scalar unit.
-// sphere test (geometry.scm:146-171); updates closest/best on a hit
-__device__ __forceinline__ void sphere_test(const v3 o, const v3 d, const double a, const v3 c, const double rr,
-                                            const int32_t id, double& closest, int32_t& best) {
+// x / a, correctly rounded, from ia = RN(1/a) (one true division per ray
+// instead of one per root).  q0 = RN(x*ia) is within 1.5 ulp of x/a; one
+// residual step makes it faithful, and the second is Markstein's: with ia =
+// RN(1/a), q1 faithful and the residual x - a*q1 exact (fma), RN(q1 + r*ia)
+// = RN(x/a).  So the quotient is the IEEE one the reference's `/` gives,
+// for every a the scenes produce (|d|^2 far from the f64 under/overflow
+// range); 5 f64 ops instead of the 11-op division sequence.
+__device__ __forceinline__ double div_ia(const double x, const double a, const double ia) {
+    const double q0 = x * ia;
+    const double q1 = fma(fma(-q0, a, x), ia, q0);
+    return fma(fma(-q1, a, x), ia, q1);
+}
+// sphere test (geometry.scm:146-171); updates closest/best on a hit.
+// a = (dot d d), ia = 1/a (div_ia)
+__device__ __forceinline__ void sphere_test(const v3 o, const v3 d, const double a, const double ia, const v3 c,
+                                            const double rr, const int32_t id, double& closest, int32_t& best) {
     const v3 oc = o - c;
     const double b = dot(oc, d);
     const double cc = dot(oc, oc) - rr;
     const double disc = b * b - a * cc;
     if (disc > 0.0) {
         const double sq = sqrt(disc);
-        double t = (-b - sq) / a;
-        if (!(kTmin < t && t < closest)) t = (-b + sq) / a;
+        double t = div_ia(-b - sq, a, ia);
+        if (!(kTmin < t && t < closest)) t = div_ia(-b + sq, a, ia);
         if (kTmin < t && t < closest) { closest = t; best = id; }
     }
 }
@@ -546,7 +559,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                                                  const MSphereRec* __restrict__ msph = nullptr,
                                                  const int32_t* __restrict__ fid = nullptr) {
     constexpr int32_t kDone = INT32_MIN;
-    const double a = dot(d, d);
+    const double a = dot(d, d), ia = 1.0 / a;
     const BoxRay br = box_ray(o, d);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
@@ -554,7 +567,10 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
     // moving spheres sharing one shutter: center(time)'s (time - t0) / den is
     // the same quotient for all of them, computed once (geometry.scm:181-184)
     const double frac_shared = (!FROZEN && sc.msph_shared) ? (time - sc.msph_t0) / sc.msph_den : 0.0;
-    int sp = 0;
+    // stack pointer as an element offset (entries sit stride apart): push / pop
+    // add or subtract stride instead of multiplying the depth by it
+    uint32_t sp = 0;
+    const uint32_t slim = (uint32_t)lmax * stride;
     int32_t node = FROZEN ? sc.fbvh2_root : sc.bvh2_root, pend = kDone;
     float tcap = f32_up(closest);                              // box t range, updated after each leaf
 #ifdef RT_STATS
@@ -571,7 +587,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
             if (node < 0) {                                   // a leaf
                 if (pend != kDone) break;                     // one is already parked
                 pend = node;
-                node = sp ? stack_ref(lstk[--sp * stride]) : kDone;
+                node = sp ? stack_ref(lstk[sp -= stride]) : kDone;
             } else {
 #ifdef RT_STATS
                 ++n_node;
@@ -582,14 +598,14 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 node_hit(N, br, tcap, hl, hr, tl, tr);
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
-                    if (sp < lmax) { lstk[sp * stride] = (SE)(lfirst ? N.r : N.l); ++sp; }
+                    if (sp < slim) { lstk[sp] = (SE)(lfirst ? N.r : N.l); sp += stride; }
                     node = lfirst ? N.l : N.r;
                 } else if (hl) {
                     node = N.l;
                 } else if (hr) {
                     node = N.r;
                 } else {
-                    node = sp ? stack_ref(lstk[--sp * stride]) : kDone;
+                    node = sp ? stack_ref(lstk[sp -= stride]) : kDone;
                 }
             }
             if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
@@ -600,7 +616,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                 ++n_leaf; ++n_sph;
 #endif
                 const SphereRec S = fsph[~pend];
-                sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, ~pend, closest, fbest);
+                sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, ~pend, closest, fbest);
             } else {
                 const BvhLeaf L = leaves[~pend];
 #ifdef RT_STATS
@@ -612,7 +628,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                         ++n_sph;
 #endif
                         const SphereRec S = fsph[s];
-                        sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, s, closest, fbest);
+                        sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, s, closest, fbest);
                     }
                 } else {
                     for (int s = L.sb; s < L.sb + L.sn; ++s) {
@@ -620,7 +636,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                         ++n_sph;
 #endif
                         const SphereRec S = sph[s];
-                        sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                        sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
                     }
                     for (int s = L.mb; s < L.mb + L.mn; ++s) {
 #ifdef RT_STATS
@@ -629,7 +645,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                         const MSphereRec S = msph[s];
                         const double frac = sc.msph_shared ? frac_shared : (time - S.t0) / S.den;
                         const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                        sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                        sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
                     }
                 }
             }
@@ -665,7 +681,7 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
                                                 BezWave& W) {
-    const double a = dot(d, d);
+    const double a = dot(d, d), ia = 1.0 / a;
     const BoxRay br = box_ray(o, d);
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     const double tscale = fmax(1.0, 1.0 / sqrt(a));
@@ -715,13 +731,13 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                 const BvhLeaf L = sc.bleaf[~node];
                 for (int s = L.sb; s < L.sb + L.sn; ++s) {
                     const SphereRec S = sc.sph[s];
-                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                    sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
                 }
                 for (int s = L.mb; s < L.mb + L.mn; ++s) {
                     const MSphereRec S = sc.msph[s];
                     const double frac = (time - S.t0) / S.den;
                     const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                    sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
                 }
                 pb = L.bb; pe = L.bb + L.bn;
 #ifdef RT_STATS
@@ -921,13 +937,13 @@ __device__ __forceinline__ void group_closest(const DevScene& sc, const Group& G
     if (G.chain >= 0) chain_ray(sc.chains[G.chain], o, d);
     const int32_t base = sc.leaf_base[G.type];
     if (G.type == LEAF_SPHERE) {                       // geometry.scm:146-171
-        const double a = dot(d, d);
+        const double a = dot(d, d), ia = 1.0 / a;
         for (int s = G.begin; s < G.end; ++s) {
             const SphereRec S = sc.sph[s];
-            sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, base + s, closest, best);
+            sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, base + s, closest, best);
         }
     } else if (G.type == LEAF_MSPHERE) {               // geometry.scm:177-208
-        const double a = dot(d, d);
+        const double a = dot(d, d), ia = 1.0 / a;
         double last_t0 = 0.0, last_den = 0.0, frac = 0.0;
         bool have = false;
         for (int s = G.begin; s < G.end; ++s) {
@@ -937,7 +953,7 @@ __device__ __forceinline__ void group_closest(const DevScene& sc, const Group& G
                 last_t0 = S.t0; last_den = S.den; have = true;
             }
             const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-            sphere_test(o, d, a, cen, S.rr, base + s, closest, best);
+            sphere_test(o, d, a, ia, cen, S.rr, base + s, closest, best);
         }
     } else if (G.type == LEAF_KLEIN) {                 // geometry.scm:645-673
         if (MED) {
@@ -1255,7 +1271,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
     bool active = false, exhausted = false, trav = false;
     uint32_t k = 0, i = 0, queued = 0;
     v3 o = mk(0.0, 0.0, 0.0), d = o;
-    double tm = 0.0, a = 0.0, tscale = 1.0, closest = kTmax;
+    double tm = 0.0, a = 0.0, ia = 0.0, tscale = 1.0, closest = kTmax;
     int32_t best = -1, node = 0;
     BoxRay br{};
     BvhNode2 N{};                                   // the lane's next node, loaded one iteration ahead
@@ -1320,6 +1336,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
                     best = -1;
                     for (int g = 0; g < gb; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
                     a = dot(d, d);
+                    ia = 1.0 / a;
                     br = box_ray(o, d);
                     tscale = fmax(1.0, 1.0 / sqrt(a));
                     bez_ray(o, d, W.ray[lane]);
@@ -1358,13 +1375,13 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
                 const BvhLeaf L = sc.bleaf[~node];
                 for (int s = L.sb; s < L.sb + L.sn; ++s) {
                     const SphereRec S = sc.sph[s];
-                    sphere_test(o, d, a, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                    sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
                 }
                 for (int s = L.mb; s < L.mb + L.mn; ++s) {
                     const MSphereRec S = sc.msph[s];
                     const double frac = (tm - S.t0) / S.den;
                     const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                    sphere_test(o, d, a, cen, S.rr, bm + s, closest, best);
+                    sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
                 }
                 pb = L.bb; pe = L.bb + L.bn;
                 if (sp == 0) {
@@ -1441,6 +1458,27 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* src, const int n, con
     for (int k = threadIdx.x; k < words; k += nthreads) l[k] = g[k];
 }
 
+// Work distribution and hit-queue append of the persistent LDS kernels.
+// Block mode: a block takes kExtLdsBlock consecutive items per grid-stride
+// step and appends them with block_append (one atomic per block and class,
+// three barriers).  Wave mode (RT_EXT_WAVE_APPEND): each wave takes its own 64
+// of those items and appends with wave_append (one atomic per wave and
+// class, no barrier), so a wave is never held by a slower wave of its block.
+// Same items, same shard (blockIdx % kShards); queue order differs, images do
+// not (a path's result does not depend on its queue position).
+#ifndef RT_EXT_WAVE_APPEND
+#define RT_EXT_WAVE_APPEND 1
+#endif
+__device__ __forceinline__ uint32_t ext_first() {
+    return blockIdx.x * kExtLdsBlock + (RT_EXT_WAVE_APPEND ? (threadIdx.x & ~63u) : 0u);
+}
+__device__ __forceinline__ uint32_t ext_lid() { return RT_EXT_WAVE_APPEND ? (threadIdx.x & 63u) : threadIdx.x; }
+__device__ __forceinline__ uint32_t ext_append(const int cls, uint32_t* __restrict__ counts, const uint32_t shard_cap,
+                                               uint32_t* s_cnt) {
+    if (RT_EXT_WAVE_APPEND) return wave_append(cls, blockIdx.x & (uint32_t)(kShards - 1), counts, shard_cap);
+    return block_append<4>(cls, counts, shard_cap, s_cnt);
+}
+
 // Dynamic LDS the persistent kernels carve (host and device use the same
 // formula: the kernels check it against the allocation they were given).
 // Layout: tree nodes | leaves | sphere records [| moving spheres] | 16-bit
@@ -1504,8 +1542,8 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
     const Tree0 t0{s_nodes, s_leaves, s_sph, s_fid};
     const int LS = sc.lane_stack;
     const QMap qm = qmap(in);
-    for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
-        const uint32_t k = base + threadIdx.x;
+    for (uint32_t base = ext_first(); base < n; base += gridDim.x * kExtLdsBlock) {
+        const uint32_t k = base + ext_lid();
         int cls = -1;
         HitRec hr{};
         if (k < n) {
@@ -1524,7 +1562,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_EXTLDS_WAVES) void k_extend_lds(co
                 cls = s_cls[leaf];
             }
         }
-        const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
+        const uint32_t slot = ext_append(cls, counts, shard_cap, s_cnt);
         if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
     }
 }
@@ -1570,8 +1608,8 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
     const Tree0 t0 = ALL ? tree0_hbm(sc) : Tree0{s_nodes, s_leaves, s_sph, s_fid};
     const TreeA ta = ALL ? TreeA{s_nodes, s_leaves, s_sph, s_msph} : treeA_hbm(sc);
     const int LS = sc.lane_stack;
-    for (uint32_t base = blockIdx.x * kExtLdsBlock; base < n; base += gridDim.x * kExtLdsBlock) {
-        const uint32_t w = base + threadIdx.x;
+    for (uint32_t base = ext_first(); base < n; base += gridDim.x * kExtLdsBlock) {
+        const uint32_t w = base + ext_lid();
         int cls = -1;
         HitRec hr{};
         if (w < n) {
@@ -1592,7 +1630,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
                 cls = s_cls[leaf];
             }
         }
-        const uint32_t slot = block_append<4>(cls, counts, shard_cap, s_cnt);
+        const uint32_t slot = ext_append(cls, counts, shard_cap, s_cnt);
         if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
     }
 }
@@ -1997,33 +2035,45 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
+#ifndef RT_FINISH_WAVES
+#define RT_FINISH_WAVES 4             // plain-sphere tails without Perlin / light mixture: 128 VGPRs, 4 waves per SIMD
+#endif                                // (the compiler's choice is 143: 3 waves; the other variants would spill at 128)
 template <int F, bool PN, bool LSM>
-__global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
+constexpr int finish_waves() { return (F == 0 && !PN && !LSM) ? RT_FINISH_WAVES : 1; }
+template <int F, bool PN, bool LSM, bool SOLO = false>
+__global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
                                                 const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
-    // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack), then, if
-    // tree0_lds, the time-0 tree (nodes, leaves, sphere records) as in
-    // k_extend_lds, then, for scenes with Perlin tables, the tables
+    // dynamic LDS: per-lane BVH stack (256 x sc.lane_stack; 16-bit entries
+    // for SOLO), then, if tree0_lds, the time-0 tree (nodes, leaves, sphere
+    // records) as in k_extend_lds, then, for scenes with Perlin tables, the
+    // tables.  SOLO (the world is one sphere BVH, DevScene::bvh_solo, with the
+    // tree in LDS): the closest hit is k_extend_lds's — direct leaves, no leaf
+    // records, 16-bit stack — so the tail carries no group loop.
     extern __shared__ uint4 s_fdyn[];
     uint32_t* s_lstack = reinterpret_cast<uint32_t*>(s_fdyn);
+    uint16_t* s_lstack16 = reinterpret_cast<uint16_t*>(s_fdyn);
     const int LS = sc.lane_stack;
     constexpr bool BEZ = (F & kFeatCurves) != 0;
     constexpr bool MED = (F & kFeatExtra) != 0;
+    static_assert(!SOLO || F == 0, "SOLO tails are plain-sphere scenes");
     __shared__ BezWave s_bw[BEZ ? 4 : 1];
-    const int words = (256 * (LS > 0 ? LS : 1) + 3) / 4;               // stack size in uint4
-    const size_t tree_words = tree0_lds ? ((size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
+    const int words = SOLO ? (256 * (LS > 0 ? LS : 1) * 2 + 15) / 16            // stack size in uint4
+                           : (256 * (LS > 0 ? LS : 1) + 3) / 4;
+    const int tl_leaves = SOLO ? 0 : sc.n_fbleaf;
+    const size_t tree_words = tree0_lds ? ((size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)tl_leaves * sizeof(BvhLeaf) +
                                            (size_t)sc.n_fsph * sizeof(SphereRec)) / 16 : 0;
     PerlinLds& P = *reinterpret_cast<PerlinLds*>(s_fdyn + words + tree_words);
     Tree0 t0 = tree0_hbm(sc);
     if (tree0_lds) {
-        const int nn = sc.n_fbvh2, nl = sc.n_fbleaf, ns = sc.n_fsph;
+        const int nn = sc.n_fbvh2, nl = tl_leaves, ns = sc.n_fsph;
         BvhNode2* s_nodes = reinterpret_cast<BvhNode2*>(s_fdyn + words);
         BvhLeaf* s_leaves = reinterpret_cast<BvhLeaf*>(s_nodes + nn);
         SphereRec* s_sph = reinterpret_cast<SphereRec*>(s_leaves + nl);
         stage_lds(s_nodes, sc.fbvh2, nn, 256);
-        stage_lds(s_leaves, sc.fbleaf, nl, 256);
+        if (!SOLO) stage_lds(s_leaves, sc.fbleaf, nl, 256);
         stage_lds(s_sph, sc.fsph, ns, 256);
         t0 = Tree0{s_nodes, s_leaves, s_sph, sc.fid};
         __syncthreads();
@@ -2063,8 +2113,12 @@ __global__ __launch_bounds__(256) void k_finish(const DevScene* __restrict__ scp
             ++segs;
             Rng g;
             if (MED) g.init(rp.k0, rp.k1, p.pix, p.smp, p.rng);
-            const int32_t leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
-                                                &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, t0, treeA_hbm(sc));
+            int32_t leaf;
+            if constexpr (SOLO)
+                leaf = closest_hit_lds<true>(sc, p.o, p.d, p.time, t, s_lstack16 + threadIdx.x, LS, t0, treeA_hbm(sc));
+            else
+                leaf = closest_hit<F>(sc, p.o, p.d, p.time, t, s_lstack + threadIdx.x, LS,
+                                      &s_bw[BEZ ? (threadIdx.x >> 6) : 0], &g, t0, treeA_hbm(sc));
             if (MED) p.rng = g.ctr;
             v3 L;
             bool cont = false;
@@ -2119,6 +2173,10 @@ static uint32_t finish_blocks() {            // persistent tail grid (RTAMD_FINI
         return (uint32_t)(b > 0 ? b : 512);
     }();
     return v;
+}
+static bool finish_generic() {               // RTAMD_FINISH_GENERIC: the group-loop tail for SOLO scenes too (A/B, tests)
+    const char* e = std::getenv("RTAMD_FINISH_GENERIC");  // read per launch: tests switch it inside one process
+    return e != nullptr && e[0] != '0';
 }
 static int scene_features(const DevScene& sc) {
     return (sc.n_bez > 0 ? kFeatCurves : 0) | (sc.n_med > 0 || sc.n_klein > 0 ? kFeatExtra : 0);
@@ -2287,14 +2345,21 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
                          hipStream_t s) {
     uint32_t blocks = (n + 255u) / 256u;
     if (blocks > finish_blocks()) blocks = finish_blocks();   // persistent lanes refill from the path list
-    size_t lds = ((size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t) + 15) / 16 * 16;
     const size_t tree = (size_t)sc.n_fbvh2 * sizeof(BvhNode2) + (size_t)sc.n_fbleaf * sizeof(BvhLeaf) +
                         (size_t)sc.n_fsph * sizeof(SphereRec);
     const int tree0_lds = (sc.fbvh2 && tree0_budget > 0 && tree <= tree0_budget) ? 1 : 0;
-    if (tree0_lds) lds += tree;
+    // SOLO tail: plain-sphere world in one BVH, its time-0 tree in LDS, child refs within int16
+    const bool solo = tree0_lds && sc.bvh_solo && scene_features(sc) == 0 && extend_lds_bytes(sc) > 0 &&
+                      sc.n_bvh2 < 32768 && sc.n_bleaf < 32768 && !finish_generic();
+    const size_t stack_entry = solo ? sizeof(uint16_t) : sizeof(uint32_t);
+    size_t lds = ((size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * stack_entry + 15) / 16 * 16;
+    if (tree0_lds) lds += solo ? tree - (size_t)sc.n_fbleaf * sizeof(BvhLeaf) : tree;
     // the Perlin tables ride at the end of the dynamic LDS, only where they are staged (PN and tables given)
     const size_t perlin = sc.has_perlin ? sizeof(PerlinLds) : 0;
 #define RT_FINISH_F(F) RT_FINISH(F, true, true)
+#define RT_FINISH_SOLO(PN, LS) \
+    hipLaunchKernelGGL((k_finish<0, PN, LS, true>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, in, \
+                       n, seg_count, tree0_lds, depth)
 #define RT_FINISH(F, PN, LS) \
     hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, in, n, \
                        seg_count, tree0_lds, depth)
@@ -2305,7 +2370,10 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
     const bool ls = sc.light.type != LIGHT_OFF;
     switch (scene_features(sc)) {
     case 0:
-        if (pn) { if (ls) RT_FINISH(0, true, true); else RT_FINISH(0, true, false); }
+        if (solo) {
+            if (pn) { if (ls) RT_FINISH_SOLO(true, true); else RT_FINISH_SOLO(true, false); }
+            else { if (ls) RT_FINISH_SOLO(false, true); else RT_FINISH_SOLO(false, false); }
+        } else if (pn) { if (ls) RT_FINISH(0, true, true); else RT_FINISH(0, true, false); }
         else { if (ls) RT_FINISH(0, false, true); else RT_FINISH(0, false, false); }
         break;
     case 1: RT_FINISH_F(1); break;
@@ -2313,6 +2381,7 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
     default: RT_FINISH_F(3); break;
     }
 #undef RT_FINISH_F
+#undef RT_FINISH_SOLO
 #undef RT_FINISH
     return hipGetLastError();
 }
