@@ -1223,6 +1223,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         RenderParams& rp = L.rp;
         rp = RenderParams{};
         rp.nx = (uint32_t)nx; rp.ny = (uint32_t)ny; rp.npix = npix;
+        rp.inx = 1.0 / (double)nx; rp.iny = 1.0 / (double)ny;
         rp.spp0 = (uint32_t)(spp_begin + done); rp.k0 = k0; rp.k1 = k1;
         rp.pixlist = s->pixlist.as<const uint32_t>();
         rp.sb = L.sb.as<double>();

@@ -209,6 +209,7 @@ struct RenderParams {
     double* sb;               // sample colours [B][3] (one rgb record per work id), B = npix * chunk_spp
     uint32_t B;
     uint32_t compact;         // accumulator indexed by shard pixel q (rt_render_shard_device), not image pixel j
+    double inx, iny;          // RN(1/nx), RN(1/ny): trace-all's (/ (+ i r) nx) as div_ia (rt_kernels.hip)
 };
 
 }  // namespace rtamd
