@@ -259,9 +259,17 @@ def main():
     from rtamd import gpu, scenes
     from rtamd._lib import call
 
+    # RCCL ("nccl") over xGMI, one GPU per rank.  RTAMD_DIST_BACKEND=gloo rehearses the
+    # multi-process flow on fewer GPUs than ranks (ranks share devices, the gather goes
+    # through host memory); it is never the measured configuration.
+    backend = os.environ.get("RTAMD_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     nx, ny, spp = a.nx, a.ny, a.spp
     scene = scenes.SCENES[a.scene](nx, ny)
     ctx = gpu.default_context(local)
@@ -316,8 +324,9 @@ def main():
             iso = step()
         finally:
             del os.environ["RTAMD_LANES"]
-    tot = torch.tensor([segs, paths], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    red_dev = "cpu" if backend == "gloo" else "cuda"
+    tot = torch.tensor([segs, paths], dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -387,7 +396,8 @@ def main():
             "config": {"workload": "%s: %s scene %dx%dx%dspp, one full frame per step"
                                    % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp),
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
-                       "parallelism": "tile-shard%d" % world if world > 1 else "single"},
+                       "parallelism": ("tile-shard%d" % world if world > 1 else "single") +
+                                      ("" if world == 1 or backend == "nccl" else " (%s rehearsal)" % backend)},
             "roofline": roof, "roofline_isolated": roof_iso, "valu": valu, "valu_issue": valu_issue,
             "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated", a.scene),
             "scene_device": scene_device(gpu.scene_info(h)),

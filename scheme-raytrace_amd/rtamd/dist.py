@@ -42,11 +42,14 @@ def gather_frame(local, nx, ny, rank, world, group=None):
     if local.numel() != 3 * counts[rank]:
         raise ValueError("rank %d holds %d values, its shard has %d pixels" % (rank, local.numel(), counts[rank]))
     width = 3 * max(counts)                     # collectives move equal-size buffers: pad to the largest shard
-    send = local
+    # RCCL gathers device buffers; gloo (CPU tests, one-GPU rehearsals of the
+    # multi-process bench) gathers host copies
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else local.device
+    send = local.to(dev)
     if local.numel() < width:
-        send = torch.zeros(width, dtype=local.dtype, device=local.device)
-        send[:local.numel()] = local
-    bufs = [torch.empty(width, dtype=local.dtype, device=local.device) for _ in range(world)] if rank == 0 else None
+        send = torch.zeros(width, dtype=local.dtype, device=dev)
+        send[:local.numel()] = local.to(dev)
+    bufs = [torch.empty(width, dtype=local.dtype, device=dev) for _ in range(world)] if rank == 0 else None
     dist.gather(send, gather_list=bufs, dst=0, group=group)
     if rank != 0:
         return None
@@ -54,7 +57,7 @@ def gather_frame(local, nx, ny, rank, world, group=None):
     rows = frame.view(-1, 3)
     for r in range(world):
         idx = torch.from_numpy(pix[r]).to(local.device)
-        rows.index_copy_(0, idx, bufs[r][:3 * counts[r]].view(-1, 3))
+        rows.index_copy_(0, idx, bufs[r][:3 * counts[r]].view(-1, 3).to(local.device))
     return frame
 
 

@@ -1,0 +1,70 @@
+"""The multi-process frame on the GPU: two ranks (gloo process group, both on
+cuda:0 — the one-GPU box has no second device for RCCL) each render their
+interleaved tiles with librtamd (rt_render_shard_device, compact accumulator)
+through rtamd.dist.render_frame — bench.py's per-step call — and rank 0's
+gathered frame must equal a one-process rt_render_device frame bit for bit.
+Only the transport differs from the 8-GPU bench (gloo through host memory
+instead of RCCL over xGMI)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+NX, NY, SPP, SEED = 96, 54, 3, 0x5EED0002
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_path, wavefront):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "scheme-raytrace_amd"))
+    if wavefront:                                # the wavefront kernels, not only the tail kernel
+        os.environ["RTAMD_TAIL_PATHS"] = "0"
+        os.environ["RTAMD_TAIL_DIV"] = "1000000000"
+    import torch
+    import torch.distributed as dist
+
+    from rtamd import dist as rdist
+    from rtamd import gpu, scenes
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    scene = scenes.random_scene(NX, NY)
+    ctx = gpu.default_context(0)
+    local = torch.zeros(rdist.local_size(NX, NY, rank, world), dtype=torch.float64, device="cuda")
+    frame = rdist.render_frame(scene, NX, NY, 0, SPP, SEED, rank, world, local=local, ctx=ctx)
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.save(out_path, frame.cpu().numpy())
+    else:
+        assert frame is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,wavefront", [(2, True), (3, False)])
+def test_multiprocess_tile_shards_equal_one_process_frame(gpu_ctx, tmp_path, monkeypatch, world, wavefront):
+    import torch
+    from rtamd import gpu, scenes
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out, wavefront), nprocs=world, join=True)
+    if wavefront:
+        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    full = torch.zeros(NX * NY * 3, dtype=torch.float64, device="cuda")
+    gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(np.load(out), full.cpu().numpy())
