@@ -289,6 +289,7 @@ struct BvhBuild {
     int leaf_max = 2;                 // RTAMD_BVH_LEAF
     bool singles = false;             // split down to one primitive per leaf even where SAH would stop
     double trav_cost = 0.5;           // RTAMD_BVH_CT: node visit cost relative to one primitive test
+    int sweep_max = 0;                // RTAMD_BVH_SWEEP: nodes of at most this many primitives use the exact SAH sweep
     static constexpr int kBins = 16;
 
     static double area(const double* lo, const double* hi) {
@@ -313,6 +314,38 @@ struct BvhBuild {
         for (int i = b; i < e; ++i) { grow(lo, hi, refs[i].lo, refs[i].hi); grow(clo, chi, refs[i].c, refs[i].c); }
         const int n = e - b;
         if (n <= leaf_max || depth >= kLaneStack - 2) return make_leaf(node, b, e, lo, hi);
+        if (n <= sweep_max) {                        // exact SAH: every split position on all three axes
+            int best_axis = -1, best_i = -1;
+            double best = 1e300;
+            std::vector<int> ord(n);
+            std::vector<double> right(n + 1);
+            for (int ax = 0; ax < 3; ++ax) {
+                for (int i = 0; i < n; ++i) ord[i] = b + i;
+                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return refs[x].c[ax] < refs[y].c[ax]; });
+                double rlo[3] = {1e300, 1e300, 1e300}, rhi[3] = {-1e300, -1e300, -1e300};
+                for (int i = n - 1; i >= 1; --i) { grow(rlo, rhi, refs[ord[i]].lo, refs[ord[i]].hi); right[i] = area(rlo, rhi); }
+                double llo[3] = {1e300, 1e300, 1e300}, lhi[3] = {-1e300, -1e300, -1e300};
+                for (int i = 1; i < n; ++i) {        // left = ord[0, i), right = ord[i, n)
+                    grow(llo, lhi, refs[ord[i - 1]].lo, refs[ord[i - 1]].hi);
+                    const double c = area(llo, lhi) * i + right[i] * (n - i);
+                    if (c < best) { best = c; best_axis = ax; best_i = i; }
+                }
+            }
+            // no finite cost (unbounded / NaN boxes, e.g. a degenerate shutter): the binned path's median split
+            if (best_axis >= 0) {
+                const double parent = area(lo, hi);
+                const bool worth = parent <= 0 || trav_cost + best / parent < (double)n;
+                if (!worth && n <= 2 * leaf_max && !singles) return make_leaf(node, b, e, lo, hi);
+                std::stable_sort(refs.begin() + b, refs.begin() + e,
+                                 [&](const PrimRef& x, const PrimRef& y) { return x.c[best_axis] < y.c[best_axis]; });
+                const int l = build(b, b + best_i, depth + 1);
+                const int r = build(b + best_i, e, depth + 1);
+                BvhNode& N = nodes[node];
+                for (int k = 0; k < 3; ++k) { N.lo[k] = lo[k]; N.hi[k] = hi[k]; }
+                N.a = l; N.b = r; N.c = -1; N.d = best_axis;
+                return node;
+            }
+        }
         int axis = 0;
         for (int k = 1; k < 3; ++k) if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
         const double ext = chi[axis] - clo[axis];
@@ -378,6 +411,16 @@ void pad_box(double* lo, double* hi) {
     for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
     const double pad = 1e-8 * m;
     for (int k = 0; k < 3; ++k) { lo[k] -= pad; hi[k] += pad; }
+}
+
+// Nodes of at most this many primitives take the exact SAH split (every
+// position on all three axes) instead of 16 bins on the widest axis: sphere
+// trees (hundreds of primitives) throughout — C2 extend -2 %, +1.1 % frame
+// (profiles/r02/ab/ab_sweep*.log); curve trees (2^20 primitives) keep the
+// binned build, whose cost stays linear per level.  RTAMD_BVH_SWEEP overrides.
+int bvh_sweep_max(const bool curves) {
+    const char* e = std::getenv("RTAMD_BVH_SWEEP");
+    return e ? std::atoi(e) : (curves ? 0 : 1 << 16);
 }
 
 size_t bvh_min_prims() {
@@ -576,6 +619,8 @@ int commit_scene(Scene* s, int world) {
                           ? 2 : 1;
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("RTAMD_BVH_CT")) bb.trav_cost = std::atof(e);
+        bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
+                                     std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));
         bb.build(0, (int)refs.size(), 0);
         // leaf ranges: refs order -> sphere / moving-sphere / curve array indices
         std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0), nb(refs.size() + 1, 0);
@@ -654,6 +699,7 @@ int commit_scene(Scene* s, int world) {
             BvhBuild b0{refs0, {}};
             b0.leaf_max = bb.leaf_max;
             b0.trav_cost = bb.trav_cost;
+            b0.sweep_max = bb.sweep_max;
             b0.singles = b0.leaf_max == 1;           // direct leaves (below) need one sphere per leaf
             b0.build(0, (int)refs0.size(), 0);
             // fsph in refs0 order; each entry remembers which sphere / moving sphere it is
