@@ -34,14 +34,14 @@ METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector spec (FMA = 2 flops)
 # Algorithmic HBM bytes of the extend kernels: every segment
-# reads its ray record o, d (6 x f64 = 48 B); a hit writes t (8) + leaf id (4)
-# + its queue entry (4) = 16 B; a miss instead reads throughput + work id
-# (28 B) and writes the sample colour (24 B) = 52 B, i.e. 36 B more.  Per
-# path add the camera ray's time (8 B, depth-0 state) and one miss (each path
-# ends in the sky except the few absorbed / depth-capped ones: an upper bound
-# within ~1%).
+# reads its ray record o, d (6 x f64 = 48 B; k_camera writes it instead); a
+# hit writes its queue record t (8) + leaf id (4) + slot (4) = 16 B; a miss
+# instead reads throughput + work id (28 B) and writes the sample colour
+# (24 B) = 52 B, i.e. 36 B more.  Per path add the camera ray's time and draw
+# counter (12 B, depth-0 state) and one miss (each path ends in the sky except
+# the few absorbed / depth-capped ones: an upper bound within ~1%).
 EXTEND_BYTES_PER_SEGMENT = 48 + 16
-EXTEND_BYTES_PER_PATH = 8 + (52 - 16)
+EXTEND_BYTES_PER_PATH = 12 + (52 - 16)
 
 
 def extend_bytes(segments, paths):
@@ -49,12 +49,12 @@ def extend_bytes(segments, paths):
 
 
 # Algorithmic HBM bytes of the wavefront shade phase (the per-material k_shade
-# launches of an iteration): a shaded hit reads its queue entry (4), hit record
-# (16) and ray record (48), plus the camera ray's time and draw counter (12)
+# launches of an iteration): a shaded hit reads its queue record (16: t, leaf,
+# slot) and ray record (48), plus the camera ray's time and draw counter (12)
 # at depth 0 or the path record (32) deeper; a survivor writes ray + path
 # records (80), a path that ends at the hit writes its sample colour (24).
 def shade_bytes(hits_d0, hits, survivors):
-    return (80 * hits_d0 + 100 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
+    return (76 * hits_d0 + 96 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
 
 
 def shade_roofline(st, note, scene):
