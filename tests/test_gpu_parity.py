@@ -231,6 +231,27 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("wavefront", [False, True])
+def test_sah_builders_same_image_bitwise(gpu_ctx, monkeypatch, wavefront):
+    """The exact-sweep SAH tree (default for sphere trees) and the binned
+    one (RTAMD_BVH_SWEEP=0) only cull differently: same image, bit for bit,
+    through the tail kernel and through the wavefront kernels."""
+    nx, ny, spp = 64, 40, 4
+    if wavefront:
+        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
+        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    imgs = []
+    for sweep in ("0", None):
+        if sweep is None:
+            monkeypatch.delenv("RTAMD_BVH_SWEEP", raising=False)
+        else:
+            monkeypatch.setenv("RTAMD_BVH_SWEEP", sweep)
+        a = np.zeros(nx * ny * 3)
+        gpu.render_host(scenes.random_scene(nx, ny), nx, ny, 0, spp, SEED, a)
+        imgs.append(a)
+    assert np.array_equal(imgs[0], imgs[1])
+
+
 def _moving_mix_scene(nx, ny):
     """Moving spheres whose shutters do not start at 0 (center(0) is an
     extrapolation), a degenerate shutter (t0 = t1: center(0) is NaN, never
