@@ -286,8 +286,14 @@ def main():
         rdist.render_frame(scene, nx, ny, 0, spp, a.seed, rank, world, local=local, frame=frame, ctx=ctx)
         return gpu.stats(h)
 
-    for _ in range(a.warmup):
+    def progress(msg):                 # a line per frame: long configurations (C5) take a minute per frame
+        if rank == 0:
+            print("bench: %s (%.1f s)" % (msg, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+
+    t_start = time.perf_counter()
+    for w in range(a.warmup):
         step()
+        progress("warmup frame %d/%d" % (w + 1, a.warmup))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -297,8 +303,9 @@ def main():
     launches = 0
     tail_segs = 0
     sh_d0 = sh = sh_surv = 0
-    for _ in range(a.steps):
+    for k in range(a.steps):
         s = step()
+        progress("timed frame %d/%d" % (k + 1, a.steps))
         segs += s.segments
         paths += s.paths
         ms_ext += s.ms_extend
@@ -324,6 +331,7 @@ def main():
             iso = step()
         finally:
             del os.environ["RTAMD_LANES"]
+        progress("single-lane profiling frame")
     red_dev = "cpu" if backend == "gloo" else "cuda"
     tot = torch.tensor([segs, paths], dtype=torch.float64, device=red_dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
