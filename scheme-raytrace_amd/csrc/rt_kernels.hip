@@ -394,6 +394,87 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
     return true;
 }
 
+// The walk of bezier_test as a per-lane state machine (stage B of the batched
+// curve tests): one node per call, so a lane whose curve is finished can take
+// the next survivor while the others keep walking.  Same nodes, same order,
+// same arithmetic as bezier_test.
+struct BezWalk {
+    Bez4 root, c;
+    double best, tmax, w1, w2;
+    int L, leaf_level;
+    uint32_t idx, it, cap;
+    bool fresh, found;
+};
+// set up the walk of curve B for t-max tmax; false if the whole curve is culled
+__device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax) {
+    bez_load(B, R, s.root);
+    s.w1 = B.w1; s.w2 = B.w2; s.tmax = tmax;
+    if (bez_culled(s.root, s.w1, tmax)) return false;
+    double l0 = -kTmax;                                         // flatness -> subdivision depth (:180-193)
+    {
+        const Bez4& c = s.root;
+        const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
+        l0 = fmax(fmax(x0, y0), l0);
+        const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
+        l0 = fmax(fmax(x1, y1), l0);
+    }
+    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / B.eps8) / log(4.0);
+    int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
+    if (maxd > kBezMaxDepth) maxd = kBezMaxDepth;
+    s.leaf_level = maxd + 1;
+    s.cap = 4u << s.leaf_level;
+    s.c = s.root; s.L = 0; s.idx = 0; s.it = 0; s.fresh = true; s.found = false; s.best = tmax;
+    return true;
+}
+// one node of the walk; true once the walk is over
+__device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
+    if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
+    if (!s.fresh) {
+        s.c = s.root;
+        for (int k = s.L - 1; k >= 0; --k) {
+            Bez4 l, r;
+            bez_split(s.c, l, r);
+            s.c = ((s.idx >> k) & 1u) ? r : l;
+        }
+    }
+    s.fresh = false;
+    const Bez4& c = s.c;
+    if (!bez_culled(c, s.w1, s.best)) {
+        if (s.L < s.leaf_level) {                               // split, left first (:167-175)
+            Bez4 l, r;
+            bez_split(c, l, r);
+            s.c = l; ++s.L; s.idx <<= 1; s.fresh = true;
+            return false;
+        }
+        // leaf segment (:130-166)
+        const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
+        const v3 dir = c.p3 - c.p0;
+        v3 dp0 = bez_tan(c, false);
+        if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
+        if (!(dot2d(dp0, c.p0 * -1.0) < 0.0)) {
+            v3 dpn = bez_tan(c, true);
+            if (dot2d(dir, dpn) < 0.0) dpn = dpn * -1.0;
+            if (!(dot2d(dpn, c.p3) < 0.0)) {
+                double w = dir.x * dir.x + dir.y * dir.y;
+                if (w != 0.0) {
+                    w = (c.p0.x * dir.x + c.p0.y * dir.y) / (-w);
+                    w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
+                    const double v = v0 * (1.0 - w) + vn * w;
+                    const v3 p = bez_point(c, v);                 // sub-curve at the global v (Q11)
+                    if (!(p.x * p.x + p.y * p.y >= s.w2 || p.z <= 0.0001 || s.tmax < p.z)) {
+                        if (!s.found || p.z < s.best) s.best = p.z;
+                        s.found = true;
+                    }
+                }
+            }
+        }
+    }
+    while (s.L > 0 && (s.idx & 1u)) { --s.L; s.idx >>= 1; }   // climb past right children
+    if (s.L == 0) return true;
+    ++s.idx;                                                    // right sibling
+    return false;
+}
+
 #ifdef RT_STATS
 // traversal statistics (stats builds only): rays, node visits, leaf visits,
 // sphere tests, moving-sphere tests, lane inner / outer loop iterations,
@@ -418,8 +499,17 @@ __device__ unsigned long long g_stats[32];
 // curve's answer does not depend on the t-max it is tested with, beyond
 // being reported only when z <= t-max (see bezier_test), so deferring the
 // tests changes no result.
+#ifndef RT_BEZ_FLAT
+#define RT_BEZ_FLAT 1                  // stage B as a refilling per-lane walk (0: one curve per lane per pass)
+#endif
+#ifndef RT_BEZ_REFILL
+#define RT_BEZ_REFILL 8                // idle lanes that take the next survivors together
+#endif
 constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
-constexpr int kBezS = 64 + kBezQ;     // survivors: < 64 carried over + one stage A's worth
+#ifndef RT_BEZ_HOLD
+#define RT_BEZ_HOLD 192                // stage B runs once this many root-cull survivors wait (multiple of 64)
+#endif
+constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
 struct BezWave {
     BezRay ray[64];                 // owner lane's ray-space matrix
     double cl[64];                  // owner's closest t when a batch runs
@@ -472,6 +562,42 @@ template <bool TRACK = false>
 __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
+#if RT_BEZ_FLAT
+    // Lanes take survivors one after the other from a wave-uniform cursor and
+    // walk them a node per iteration (BezWalk): when at least RT_BEZ_REFILL
+    // lanes are idle they take the next survivors together, so a lane is not
+    // held by the longest walk of a fixed batch of 64.
+    {
+        BezWalk wk;
+        bool busy = false;
+        uint32_t si = 0, cursor = 0;
+        const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * ((4ull << (kBezMaxDepth + 1)) + 2ull);
+        for (unsigned long long g = 0;; ++g) {                    // wave-uniform
+            if (g > guard_cap) { raise_fault(RT_FAULT_CURVE); break; }
+            const unsigned long long idle = __ballot(!busy);
+            if (cursor < nb && (__popcll(idle) >= RT_BEZ_REFILL || idle == act)) {
+                if (!busy) {
+                    const uint32_t i = cursor + lanes_below(idle);
+                    if (i < nb) {
+                        const uint32_t e = W.sv[i];
+                        si = i;
+                        busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
+                        if (!busy) W.sz[i] = INFINITY;            // culled at the root
+                    }
+                }
+                cursor += (uint32_t)__popcll(idle);
+            }
+            if (__ballot(busy) == 0ull) {
+                if (cursor >= nb) break;
+                continue;
+            }
+            if (busy && bez_walk_step(wk)) {
+                W.sz[si] = (wk.found && kTmin < wk.best) ? wk.best : INFINITY;   // :201
+                busy = false;
+            }
+        }
+    }
+#else
     for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
         if (i < nb) {
@@ -480,6 +606,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             W.sz[i] = bezier_test(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], t) ? t : INFINITY;
         }
     }
+#endif
     wave_sync();
     for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
@@ -1418,7 +1545,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
             wave_sync();
             svn = bez_stage_a<true>(sc, W, qn, svn);
             qn = 0;
-            const uint32_t nb = more ? svn - svn % 64u : svn;
+            const uint32_t nb = more ? (svn >= (uint32_t)RT_BEZ_HOLD ? svn - svn % 64u : 0u) : svn;
             if (nb > 0u) {
                 W.hz[lane] = INFINITY;
                 W.hid[lane] = 0xFFFFFFFFu;
