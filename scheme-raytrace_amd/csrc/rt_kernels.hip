@@ -405,23 +405,25 @@ struct BezWalk {
     uint32_t idx, it, cap;
     bool fresh, found;
 };
-// set up the walk of curve B for t-max tmax; false if the whole curve is culled
-__device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax) {
+// converge's subdivision depth from the transformed curve's flatness (:180-193)
+__device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
+    double l0 = -kTmax;
+    const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
+    l0 = fmax(fmax(x0, y0), l0);
+    const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
+    l0 = fmax(fmax(x1, y1), l0);
+    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / eps8) / log(4.0);
+    const int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
+    return maxd > kBezMaxDepth ? kBezMaxDepth : maxd;
+}
+// set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
+// stage A's root cull) is given; false if the whole curve is culled
+__device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
+                                               const int leaf_level) {
     bez_load(B, R, s.root);
     s.w1 = B.w1; s.w2 = B.w2; s.tmax = tmax;
     if (bez_culled(s.root, s.w1, tmax)) return false;
-    double l0 = -kTmax;                                         // flatness -> subdivision depth (:180-193)
-    {
-        const Bez4& c = s.root;
-        const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
-        l0 = fmax(fmax(x0, y0), l0);
-        const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
-        l0 = fmax(fmax(x1, y1), l0);
-    }
-    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / B.eps8) / log(4.0);
-    int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
-    if (maxd > kBezMaxDepth) maxd = kBezMaxDepth;
-    s.leaf_level = maxd + 1;
+    s.leaf_level = leaf_level;
     s.cap = 4u << s.leaf_level;
     s.c = s.root; s.L = 0; s.idx = 0; s.it = 0; s.fresh = true; s.found = false; s.best = tmax;
     return true;
@@ -519,6 +521,7 @@ struct BezWave {
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
     uint32_t done[64];              // persistent kernel: owner's candidates resolved so far
+    uint8_t lev[kBezS];             // survivors' subdivision leaf levels (stage A)
 };
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -539,13 +542,18 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
         const uint32_t i = base + rank;
         bool keep = false;
         uint32_t e = 0;
+        uint8_t lev = 0;
         if (i < qn) {
             e = W.q[i];
-            keep = bez_root_passes(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
+            const BezierRec& B = sc.bez[e >> 6];
+            Bez4 c;
+            bez_load(B, W.ray[e & 63u], c);
+            keep = !bez_culled(c, B.w1, W.cl[e & 63u]);
+            if (keep) lev = (uint8_t)(bez_maxd(c, B.eps8) + 1);
             if (TRACK && !keep) atomicAdd(&W.done[e & 63u], 1u);
         }
         const unsigned long long m = __ballot(keep);
-        if (keep) W.sv[svn + lanes_below(m)] = e;
+        if (keep) { W.sv[svn + lanes_below(m)] = e; W.lev[svn + lanes_below(m)] = lev; }
         svn += (uint32_t)__popcll(m);
 #ifdef RT_STATS
         if (rank == 0) RT_STAT(15, __popcll(m));
@@ -581,7 +589,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (i < nb) {
                         const uint32_t e = W.sv[i];
                         si = i;
-                        busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u]);
+                        busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
                         if (!busy) W.sz[i] = INFINITY;            // culled at the root
                     }
                 }
@@ -625,9 +633,10 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
     wave_sync();
     const uint32_t rest = svn - nb;             // < nact <= 64, disjoint from [0, rest) only if nb >= rest
     uint32_t e = 0;
-    if (rank < rest) e = W.sv[nb + rank];
+    uint8_t lv = 0;
+    if (rank < rest) { e = W.sv[nb + rank]; lv = W.lev[nb + rank]; }
     wave_sync();
-    if (rank < rest) W.sv[rank] = e;
+    if (rank < rest) { W.sv[rank] = e; W.lev[rank] = lv; }
     wave_sync();
 }
 
