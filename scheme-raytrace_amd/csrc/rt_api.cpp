@@ -123,6 +123,7 @@ struct Lane {
 
 struct Scene {
     int ctx = -1;
+    size_t pool_cap = 0;                       // paths per chunk (max_paths), fixed at the first render
     std::vector<DevTexture> texs;
     std::vector<DevMaterial> mats;
     std::vector<Obj> objs;
@@ -1031,10 +1032,26 @@ std::string fault_text(uint32_t f) {
     return m;
 }
 
-size_t max_paths() {
-    const char* e = std::getenv("RTAMD_MAX_PATHS");
-    size_t v = e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)96 << 20;
-    return v < 1024 ? 1024 : v;
+// Path-pool cap (paths per chunk).  Bigger pools mean fewer chunks, each
+// with its own narrow tail: C2 (1920x1080x1024 spp) 13 383 Mrays/s with 96M
+// paths (22 chunks), 13 675 with 200M (12), 13 742 with 330M (8 chunks;
+// profiles/r02/pool/).  Default 288M paths, but at most what lets the render
+// lanes' pools (~272 B per path: two path-state pools, four hit queues, the
+// sample buffer) take 55 % of the device's free memory.  RTAMD_MAX_PATHS overrides.
+size_t max_paths(const int lanes) {
+    if (const char* e = std::getenv("RTAMD_MAX_PATHS")) {
+        const size_t v = (size_t)std::strtoull(e, nullptr, 10);
+        return v < 1024 ? 1024 : v;
+    }
+    size_t v = (size_t)288 << 20;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+        const size_t fit = free_b / 100 * 55 / ((size_t)std::max(1, lanes) * 272);
+        if (fit < v) v = fit;
+    } else {
+        (void)hipGetLastError();
+    }
+    return v < ((size_t)1 << 20) ? ((size_t)1 << 20) : v;
 }
 
 int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = no overlap)
@@ -1111,7 +1128,9 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // Chunks of samples: as few as the pool cap allows, but at least four and
     // an even count when the samples allow, so two render lanes end together
     // (a frame of three chunks would leave one lane alone for a third of it).
-    const size_t cap_paths = max_paths();
+    // the cap is sized on the scene's first render (before its own pools exist), then kept
+    if (!s->pool_cap || std::getenv("RTAMD_MAX_PATHS")) s->pool_cap = max_paths(std::min(kLanes, lanes_wanted()));
+    const size_t cap_paths = s->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     {
