@@ -1070,7 +1070,8 @@ uint32_t tail_threshold() {
 }
 uint32_t tail_divisor() {
     const char* e = std::getenv("RTAMD_TAIL_DIV");
-    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 128ul;   // B/128: +2.4 % over B/64 with the 8-wave extend
+    // B/256 with 288M-path pools (+0.9 % over B/128, profiles/r02/tail*/; B/128 was best with 96M pools)
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 256ul;
     return v ? (uint32_t)v : 1u;
 }
 

@@ -1,7 +1,7 @@
 """GPU tests of the production schedule and the row / shard entry points.
 
 The small parity renders in test_gpu_parity.py fit under the tail threshold
-(max(32768, B/128) paths, rt_api.cpp tail_threshold) and so run entirely in
+(max(32768, B/256) paths, rt_api.cpp tail_threshold) and so run entirely in
 the tail kernel k_finish.  The tests here size the work so the wavefront
 kernels the benchmark times — k_camera, k_extend_lds, the per-material
 k_shade queues, sharded compaction, several sample chunks on two render
