@@ -2443,10 +2443,11 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
                         const HitBuf& hit, const QView& qv, uint32_t n_upper,
                         const PathState& out, uint32_t* out_counts, uint32_t shard_cap, uint32_t depth, hipStream_t s) {
     // grid-stride cap: each block stages the leaf records once, so fewer,
-    // longer-lived blocks (2048 measured best of 1024..8192: +1.5 % C2)
+    // longer-lived blocks (2048 was best of 1024..8192 with 96M-path pools;
+    // 1024 with the 288M-path pools: +1.5 % C2, 512 -14 %: profiles/r02/shadeb/)
     static const uint32_t max_blocks = [] {          // RTAMD_SHADE_BLOCKS (A/B)
         const char* e = std::getenv("RTAMD_SHADE_BLOCKS");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 2048ul;
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1024ul;
         return (uint32_t)(v >= 4096 ? 4096 : v >= 8 ? v / 8 * 8 : 8);   // rt_api's shard slack assumes <= 4096
     }();
     uint32_t blocks = (n_upper + 255u) / 256u;
