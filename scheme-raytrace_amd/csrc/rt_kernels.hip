@@ -338,7 +338,9 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
     // the same split sequence from the root, so every sub-curve carries the
     // exact values the reference's recursion computes.
     const Bez4 root = c;
-    const int leaf_level = maxd + 1;            // converge's depth < 0 (root level has depth maxd)
+    // converge's depth < 0 (root level has depth maxd); a negative maxd (a flat
+    // curve) makes the root a leaf, as a leaf level of 0 does
+    const int leaf_level = maxd + 1 > 0 ? maxd + 1 : 0;
     int L = 0;
     uint32_t idx = 0;
     bool fresh = true;
@@ -549,7 +551,8 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
             Bez4 c;
             bez_load(B, W.ray[e & 63u], c);
             keep = !bez_culled(c, B.w1, W.cl[e & 63u]);
-            if (keep) lev = (uint8_t)(bez_maxd(c, B.eps8) + 1);
+            // leaf level maxd + 1, at least 0: a flat curve's maxd is negative (its root is a leaf)
+            if (keep) lev = (uint8_t)max(0, bez_maxd(c, B.eps8) + 1);
             if (TRACK && !keep) atomicAdd(&W.done[e & 63u], 1u);
         }
         const unsigned long long m = __ballot(keep);

@@ -478,12 +478,19 @@ def test_wavefront_matches_tail_kernel_bitwise(gpu_ctx, monkeypatch, name):
     assert np.array_equal(a, b), np.abs(a - b).max()
 
 
-def test_curve_kernels_bitwise(gpu_ctx, monkeypatch):
+@pytest.mark.parametrize("flat_curves", [False, True])
+def test_curve_kernels_bitwise(gpu_ctx, monkeypatch, flat_curves):
     """Curves, spheres and moving spheres in one world BVH between rect
     groups, through the wavefront: the persistent curve kernel, the per-ray
-    curve kernel and the flat list give the same image bit for bit."""
+    curve kernel and the flat list give the same image bit for bit.
+    flat_curves adds short, nearly straight curves whose subdivision depth
+    ceil(log4(...)) is negative (bezier.scm:180-193: the root is a leaf); the
+    flat list's per-lane test and the batched stage A/B must agree on them.
+    (The C5 fault that the leaf-level clamp fixed did not reproduce at this
+    size, so this is a parity check for the case, not that fault's replay.)"""
     from rtamd import scene as g, vec as v
     from rtamd.rng import HostStream
+    import numpy as np
     nx, ny, spp = 40, 40, 2
     rr = HostStream(0x5EED0103)
     red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
@@ -494,6 +501,13 @@ def test_curve_kernels_bitwise(gpu_ctx, monkeypatch):
     objs = [g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, white)),
             g.make_xz_rect(0, 555, 0, 555, 0, white)]
     objs.append(g.bezier_array(scenes.random_polyline_curves(600), 3.0, red))
+    if flat_curves:                  # 20000 tiny curves through the volume, extent ~0.5: half bent
+        rs = np.random.default_rng(0x5EED0104)   # by ~1e-3 (maxd -2..-4 at width 6), half straight
+        base = rs.uniform(20.0, 535.0, size=(20000, 1, 3))      # (l0 = rounding only, maxd ~ -20)
+        t = np.linspace(0.0, 0.5, 4).reshape(1, 4, 1) * rs.normal(size=(20000, 1, 3))
+        bend = 1e-3 * rs.normal(size=(20000, 4, 3))
+        bend[:10000] = 0.0
+        objs.append(g.bezier_array((base + t + bend).reshape(20000, 12), 6.0, white))
     for i in range(40):
         c = v.vec3(60 + rr() * 430, 40 + rr() * 400, 60 + rr() * 430)
         m = (white, metal, glass)[i % 3]
