@@ -683,6 +683,45 @@ __device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, con
     hr = one(1, tr);
 }
 
+// Sign-selected slab planes (RT_SIGNED_SLAB, the LDS-tree walks): with the
+// sign of 1/d known per lane, an axis's near plane is its lo plane for a
+// positive component and its hi plane otherwise (fma(b, 1/d, -o/d) rounds
+// monotonically in b), so the per-axis min / max pairs of node_hit go away
+// and the results are node_hit's bit for bit.  SlabOff: byte offsets of the
+// near / far plane pairs (left, right) in a BvhNode2.
+#ifndef RT_SIGNED_SLAB
+#define RT_SIGNED_SLAB 1
+#endif
+struct SlabOff { uint32_t nx, ny, nz, fx, fy, fz; };
+__device__ __forceinline__ SlabOff slab_off(const BoxRay& r) {
+    SlabOff o;                                              // far = near ^ (lo ^ hi offset)
+    o.nx = r.ix < 0.0f ? 24u : 0u;  o.fx = o.nx ^ 24u;     // b[0..1] lo x, b[6..7] hi x
+    o.ny = r.iy < 0.0f ? 32u : 8u;  o.fy = o.ny ^ 40u;     // b[2..3], b[8..9]
+    o.nz = r.iz < 0.0f ? 40u : 16u; o.fz = o.nz ^ 56u;     // b[4..5], b[10..11]
+    return o;
+}
+// The six plane-pair pointers of node 0 (nodes + the SlabOff offsets) are
+// per-lane constants; node k's pair is at pointer + k * 64 (one shift-add per
+// address).
+struct SlabPtr { const char *nx, *ny, *nz, *fx, *fy, *fz; };
+__device__ __forceinline__ SlabPtr slab_ptr(const BvhNode2* nodes, const SlabOff& so) {
+    const char* B = reinterpret_cast<const char*>(nodes);
+    return SlabPtr{B + so.nx, B + so.ny, B + so.nz, B + so.fx, B + so.fy, B + so.fz};
+}
+__device__ __forceinline__ void node_hit_signed(const SlabPtr& sp, const uint32_t k, const BoxRay& r,
+                                                const float tcap, bool& hl, bool& hr, float& tl, float& tr) {
+    static_assert(sizeof(BvhNode2) == 64, "node_hit_signed addresses 64-B nodes");
+    auto pair = [&](const char* p) { return *reinterpret_cast<const float2*>(p + (k << 6)); };
+    const float2 nx = pair(sp.nx), fx = pair(sp.fx), ny = pair(sp.ny), fy = pair(sp.fy);
+    const float2 nz = pair(sp.nz), fz = pair(sp.fz);
+    tl = fmaxf(fmaxf(fmaf(nx.x, r.ix, -r.px), fmaf(ny.x, r.iy, -r.py)), fmaxf(fmaf(nz.x, r.iz, -r.pz), 0.0f));
+    tr = fmaxf(fmaxf(fmaf(nx.y, r.ix, -r.px), fmaf(ny.y, r.iy, -r.py)), fmaxf(fmaf(nz.y, r.iz, -r.pz), 0.0f));
+    const float fl = fminf(fminf(fmaf(fx.x, r.ix, -r.px), fmaf(fy.x, r.iy, -r.py)), fminf(fmaf(fz.x, r.iz, -r.pz), tcap));
+    const float fr = fminf(fminf(fmaf(fx.y, r.ix, -r.px), fmaf(fy.y, r.iy, -r.py)), fminf(fmaf(fz.y, r.iz, -r.pz), tcap));
+    hl = tl <= fl;
+    hr = tr <= fr;
+}
+
 // FROZEN: the time-0 tree (DevScene::fbvh2), whose leaves hold plain sphere
 // records (moving spheres at center(0)); otherwise the all-times tree.
 // nodes / leaves / fsph may point into LDS (k_extend_lds) or HBM.
@@ -705,6 +744,9 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d), ia = 1.0 / a;
     const BoxRay br = box_ray(o, d);
+    // 16-bit stacks: the LDS-tree walks; RT_SIGNED_SLAB 1 = the time-0 tree only, 2 = also the all-times tree
+    constexpr bool SIGNED = sizeof(SE) == 2 && (RT_SIGNED_SLAB == 2 || (RT_SIGNED_SLAB == 1 && FROZEN));
+    const SlabPtr slp = slab_ptr(nodes, slab_off(br));
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int32_t fbest = -1;                                       // FROZEN: fsph index of the best hit
@@ -736,18 +778,25 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
 #ifdef RT_STATS
                 ++n_node;
 #endif
-                const BvhNode2 N = nodes[node];
                 float tl, tr;
                 bool hl, hr;
-                node_hit(N, br, tcap, hl, hr, tl, tr);
+                int2 N;                                       // child refs (l, r)
+                if constexpr (SIGNED) {
+                    node_hit_signed(slp, (uint32_t)node, br, tcap, hl, hr, tl, tr);
+                    N = *reinterpret_cast<const int2*>(&nodes[node].l);
+                } else {
+                    const BvhNode2 M = nodes[node];
+                    node_hit(M, br, tcap, hl, hr, tl, tr);
+                    N = make_int2(M.l, M.r);
+                }
                 if (hl && hr) {
                     const bool lfirst = tl <= tr;
-                    if (sp < slim) { lstk[sp] = (SE)(lfirst ? N.r : N.l); sp += stride; }
-                    node = lfirst ? N.l : N.r;
+                    if (sp < slim) { lstk[sp] = (SE)(lfirst ? N.y : N.x); sp += stride; }
+                    node = lfirst ? N.x : N.y;
                 } else if (hl) {
-                    node = N.l;
+                    node = N.x;
                 } else if (hr) {
-                    node = N.r;
+                    node = N.y;
                 } else {
                     node = sp ? stack_ref(lstk[sp -= stride]) : kDone;
                 }
