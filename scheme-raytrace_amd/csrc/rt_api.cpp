@@ -43,6 +43,15 @@ hipError_t take_fault(uint32_t*);
 using namespace rtamd;
 
 namespace {
+// share (percent, env; default all) of a persistent kernel's resident blocks
+// it is launched with: fewer leave room for the other lane's kernels (A/B)
+uint32_t grid_share(const uint32_t resident, const char* env) {
+    const char* e = std::getenv(env);
+    const unsigned long pct = e ? std::strtoul(e, nullptr, 10) : 100ul;
+    if (pct >= 100ul) return resident;
+    const uint32_t b = (uint32_t)((uint64_t)resident * (pct ? pct : 1ul) / 100ul) / 8u * 8u;
+    return b >= 8u ? b : 8u;
+}
 
 thread_local std::string g_err;
 int fail(const std::string& msg) { g_err = msg; return 1; }
@@ -980,7 +989,7 @@ int commit_scene(Scene* s, int world) {
         uint32_t mb = 0;
         if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
             s->ext_lds = lds;
-            s->ext_lds_blocks = mb;
+            s->ext_lds_blocks = grid_share(mb, "RTAMD_EXT_PCT");
         }
         (void)hipGetLastError();
     }
@@ -991,7 +1000,7 @@ int commit_scene(Scene* s, int world) {
         uint32_t mb = 0;
         if (lds > 0 && lds <= extend_lds_budget() && camera_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
             s->cam_lds = lds;
-            s->cam_blocks = mb;
+            s->cam_blocks = grid_share(mb, "RTAMD_CAM_PCT");
         }
         (void)hipGetLastError();
     }

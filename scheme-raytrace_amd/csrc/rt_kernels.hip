@@ -692,6 +692,9 @@ __device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, con
 #ifndef RT_SIGNED_SLAB
 #define RT_SIGNED_SLAB 1
 #endif
+#ifndef RT_SEARCH_MAX
+#define RT_SEARCH_MAX 0                // the walk's leaf phase starts once at most this many lanes lack a parked leaf
+#endif
 struct SlabOff { uint32_t nx, ny, nz, fx, fy, fz; };
 __device__ __forceinline__ SlabOff slab_off(const BoxRay& r) {
     SlabOff o;                                              // far = near ^ (lo ^ hi offset)
@@ -801,7 +804,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                     node = sp ? stack_ref(lstk[sp -= stride]) : kDone;
                 }
             }
-            if (__ballot(pend == kDone) == 0ull) break;       // every active lane has a leaf parked
+            // every active lane has a leaf parked (RT_SEARCH_MAX: or at most that many still search)
+            if ((uint32_t)__popcll(__ballot(pend == kDone)) <= (uint32_t)RT_SEARCH_MAX) break;
         }
         if (pend != kDone) {
             if constexpr (DIRECT) {
