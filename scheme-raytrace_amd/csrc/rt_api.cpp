@@ -1135,17 +1135,24 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     }
     const uint32_t npix = s->pix_n;
     if (npix == 0) return 0;
-    // Chunks of samples: as few as the pool cap allows, but at least four and
-    // an even count when the samples allow, so two render lanes end together
-    // (a frame of three chunks would leave one lane alone for a third of it).
+    // Chunks of samples: as few as the pool cap allows, but at least two (one
+    // per render lane) and an even count when the samples allow, so the two
+    // lanes end together (a frame of three chunks would leave one lane alone
+    // for a third of it).  A floor of four cost 6.5 % on a 1/8-frame shard
+    // (680x381x1024 spp, the per-rank work at 8 GPUs) and 2.4 % at 1/4
+    // (profiles/r02/mc/).
     // the cap is sized on the scene's first render (before its own pools exist), then kept
     if (!s->pool_cap || std::getenv("RTAMD_MAX_PATHS")) s->pool_cap = max_paths(std::min(kLanes, lanes_wanted()));
     const size_t cap_paths = s->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     {
+        static const int min_chunks = [] {          // RTAMD_MIN_CHUNKS (A/B; default 2)
+            const char* e = std::getenv("RTAMD_MIN_CHUNKS");
+            return e ? std::max(1, std::atoi(e)) : 2;
+        }();
         int n = (int)((spp_count + chunk - 1) / chunk);
-        if (n < 4) n = std::min(4, spp_count);
+        if (n < min_chunks) n = std::min(min_chunks, spp_count);
         if (n > 1 && (n & 1) && n < spp_count) ++n;
         chunk = (uint32_t)((spp_count + n - 1) / n);
     }
