@@ -38,6 +38,7 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
                              const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
+hipError_t set_reject_cap(int);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -1120,6 +1121,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     {
         uint32_t stale = 0;
         HIPCHK(take_fault(&stale));                  // a fault word left by another context's failed launch
+        const char* e = std::getenv("RTAMD_REJECT_CAP");  // tests: drive a sampler into its cap
+        HIPCHK(set_reject_cap(e ? std::max(0, std::atoi(e)) : 4096));
     }
     if (spp_count == 0) return 0;
 

@@ -44,6 +44,9 @@ namespace rtamd {
 __device__ unsigned int g_fault;
 __device__ __forceinline__ void raise_fault(const unsigned int bit) { atomicOr(&g_fault, bit); }
 constexpr int kRejectCap = 4096;               // rejection sampler attempts (P(reject) <= 0.48 per attempt)
+// the cap the samplers use: kRejectCap unless a test lowers it (RTAMD_REJECT_CAP, set_reject_cap) to
+// drive the fault path of a real sampler loop without a degenerate stream
+__device__ int g_reject_cap = kRejectCap;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;      // block_append / wave_append: the shard is full
 
 // ------------------------------------------------------------------ RNG
@@ -168,7 +171,7 @@ __device__ __forceinline__ void camera_ray(const DevScene& sc, const RenderParam
         const double a = g.next(), b = g.next();
         p = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, 0.0 * 2.0 - 0.0);
         if (dot(p, p) < 1.0) break;
-        if (it >= kRejectCap) { raise_fault(RT_FAULT_REJECT); p = mk(0.0, 0.0, 0.0); break; }
+        if (it >= g_reject_cap) { raise_fault(RT_FAULT_REJECT); p = mk(0.0, 0.0, 0.0); break; }
     }
     const v3 rd = p * c.lens;
     const v3 cu = mk(c.u[0], c.u[1], c.u[2]), cv = mk(c.v[0], c.v[1], c.v[2]);
@@ -2132,7 +2135,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
             const double a = g.next(), b = g.next(), c = g.next();
             s = mk(a * 2.0 - 1.0, b * 2.0 - 1.0, c * 2.0 - 1.0);
             if (dot(s, s) < 1.0) break;
-            if (it >= kRejectCap) { raise_fault(RT_FAULT_REJECT); s = mk(0.0, 0.0, 0.0); break; }
+            if (it >= g_reject_cap) { raise_fault(RT_FAULT_REJECT); s = mk(0.0, 0.0, 0.0); break; }
         }
         const v3 sd = reflected + s * li.mparam;
         if (!(dot(sd, nrm) > 0.0)) return false;             // absorbed: emitted 0
@@ -2582,6 +2585,18 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
 #undef RT_FINISH_SOLO
 #undef RT_FINISH
     return hipGetLastError();
+}
+// the samplers' attempt cap (render_impl: RTAMD_REJECT_CAP, tests only; default kRejectCap)
+hipError_t set_reject_cap(int cap) {
+    static int applied[64];                     // per device; 0 = not written yet (the default)
+    int dev = 0;
+    HIP_RETURN_IF(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    const int have = applied[dev] ? applied[dev] - 1 : kRejectCap;
+    if (cap == have) return hipSuccess;
+    HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_reject_cap), &cap, sizeof cap));
+    applied[dev] = cap + 1;
+    return hipSuccess;
 }
 // the device fault word: read and clear (render_impl, after the render's streams are synchronised)
 hipError_t take_fault(uint32_t* out) {

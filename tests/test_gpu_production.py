@@ -202,3 +202,32 @@ def test_noise_texture_vs_oracle(gpu_ctx, oracle_mod, monkeypatch, wavefront):
     assert np.isfinite(acc).all() and acc.sum() > 0
     assert rms <= RMS_TOL
     assert nbad <= max(2, npx // 200)
+
+
+@pytest.mark.parametrize("wavefront", [False, True])
+def test_sampler_cap_raises_fault_not_hang(gpu_ctx, monkeypatch, wavefront):
+    """Every device loop that waits on random data has an attempt cap a valid
+    stream cannot reach (rt_kernels.hip kRejectCap = 4096, P(reject) <= 0.48).
+    RTAMD_REJECT_CAP=0 lowers the cap so the real samplers — random-in-unit-disk
+    in the camera (util.scm:17-23, k_camera / k_finish) and random-in-unit-sphere
+    in metal scatter (util.scm:9-15, k_shade / k_finish) — hit it on their first
+    rejected draw: the render must return with rt_last_error naming the fault,
+    not hang, and the next render (default cap) must be clean and unchanged."""
+    import torch
+    from rtamd._lib import RtError
+    nx, ny, spp = 96, 54, 8
+    if wavefront:
+        _wavefront_only(monkeypatch)
+    scene = scenes.random_scene(nx, ny)
+    good = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    gpu.render_device(scene, nx, ny, 0, spp, SEED, good.data_ptr())
+    torch.cuda.synchronize()
+    acc = torch.zeros_like(good)
+    monkeypatch.setenv("RTAMD_REJECT_CAP", "0")
+    with pytest.raises(RtError, match="rejection sampler"):
+        gpu.render_device(scene, nx, ny, 0, spp, SEED, acc.data_ptr())
+    monkeypatch.delenv("RTAMD_REJECT_CAP")
+    acc.zero_()
+    gpu.render_device(scene, nx, ny, 0, spp, SEED, acc.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(acc, good)
