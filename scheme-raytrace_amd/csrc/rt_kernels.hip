@@ -2193,6 +2193,13 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 #endif
 template <int MAT>
 constexpr int shade_waves() { return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD : RT_SHADE_WAVES; }
+#ifndef RT_SHADE_PREFETCH
+#define RT_SHADE_PREFETCH 0
+#endif
+template <int MAT>
+constexpr bool shade_prefetch() {
+    return RT_SHADE_PREFETCH == 2 || (RT_SHADE_PREFETCH == 1 && (MAT == MAT_METAL || MAT == MAT_DIELECTRIC));
+}
 template <int MAT, bool PN, bool LS, bool LL>
 __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
                                                                 const PathState in, const HitRec* __restrict__ hq,
@@ -2214,13 +2221,22 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
     uint32_t n = 0;
 #pragma unroll
     for (int x = 0; x < kShards; ++x) n += qv.counts[x * kCntStride];
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+    // PF: the next grid-stride item's queue entry is loaded while this item is
+    // shaded, so an iteration starts with its ray / path gather instead of a
+    // dependent queue load first (RT_SHADE_PREFETCH: 1 = metal / dielectric,
+    // 2 = every material)
+    constexpr bool PF = shade_prefetch<MAT>();
+    const uint32_t gstride = gridDim.x * 256u;
+    HitRec Hn{};
+    if (PF && blockIdx.x * 256u + threadIdx.x < n) Hn = hq[qphys(qm, blockIdx.x * 256u + threadIdx.x)];
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gstride) {
         const uint32_t k = base + threadIdx.x;
         bool alive = false;
         PathRegs p;
         if (k < n) {
-            const HitRec H = hq[qphys(qm, k)];
+            const HitRec H = PF ? Hn : hq[qphys(qm, k)];
             load_path(in, H.slot, p, rp, depth);
+            if (PF && k + gstride < n) Hn = hq[qphys(qm, k + gstride)];
             v3 L;
             alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
             if (!alive) write_sample(rp, p, L);
