@@ -1021,11 +1021,20 @@ PixSel full_frame(int ny) { return PixSel{0, ny, 0, 1}; }
 std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
     const int T = 16;
     const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
+    static const bool quad = std::getenv("RTAMD_PIX_QUAD") != nullptr;   // A/B: 8x8 quads per wave
     std::vector<uint32_t> out;
     out.reserve((size_t)nx * (size_t)(ps.y1 - ps.y0) / (size_t)ps.nshard + T * T);
     for (int t = 0; t < tx * ty; ++t) {
         if (t % ps.nshard != ps.shard) continue;
         const int bx = (t % tx) * T, by = (t / tx) * T;
+        if (quad && bx + T <= nx && by + T <= ny && by >= ps.y0 && by + T <= ps.y1) {
+            // a whole tile: its four 8x8 quads in turn, so a wave's 64 pixels are a square
+            for (int q = 0; q < 4; ++q)
+                for (int yy = by + (q >> 1) * 8; yy < by + (q >> 1) * 8 + 8; ++yy)
+                    for (int xx = bx + (q & 1) * 8; xx < bx + (q & 1) * 8 + 8; ++xx)
+                        out.push_back((uint32_t)(yy * nx + xx));
+            continue;
+        }
         for (int yy = std::max(by, ps.y0); yy < std::min(std::min(by + T, ny), ps.y1); ++yy)
             for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
     }
