@@ -30,7 +30,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "scheme-raytrace_amd"))
 
-METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref"
+METRIC = "Mrays/sec at 1920x1080x1024spp RTIOW cover scene; per-pixel RMS vs ref"   # BASELINE.json (C2)
+SCENE_NAME = {"cover": "RTIOW cover scene", "cover_marble": "Perlin-textured + moving spheres cover scene",
+              "cornell": "Cornell box scene", "cornell_mixture": "Cornell box scene with pdf.scm mixture sampling",
+              "curves": "2^20 Bezier curves scene"}
+
+
+def metric_for(scene, nx, ny, spp):
+    """The metric string for this run's configuration (BASELINE.json's for C2)."""
+    return "Mrays/sec at %dx%dx%dspp %s; per-pixel RMS vs ref" % (nx, ny, spp, SCENE_NAME.get(scene, scene + " scene"))
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector spec (FMA = 2 flops)
 # Algorithmic HBM bytes of the extend kernels (DESIGN.md §5): every segment
@@ -277,7 +285,7 @@ def main():
     call("rt_set_profiling", h, 0 if a.no_profile_events else 1)
     # world == 1: the frame accumulator; world > 1: this rank's compact shard (its tiles only), gathered
     # onto rank 0 over RCCL at frame end (rtamd.dist.gather_frame)
-    frame = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda") if world == 1 else None
+    frame = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda") if world == 1 or rank == 0 else None
     local = torch.zeros(rdist.local_size(nx, ny, rank, world), dtype=torch.float64, device="cuda") \
         if world > 1 else None
 
@@ -397,7 +405,7 @@ def main():
                         "f64_flops_per_segment": round(pm["f64_flops_per_segment"], 1),
                         "note": "issued f64 lane-ops from SQ_INSTS_VALU_{ADD,MUL,FMA(x2),TRANS}_F64 x 64"}
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "metric": metric_for(a.scene, nx, ny, spp), "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: %s; path RNG seed %#x" % (SCENE_DATA.get(a.scene, a.scene + " scene"), a.seed),

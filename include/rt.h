@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -50,9 +50,16 @@ enum { RT_RECT_XY = 0, RT_RECT_XZ = 1, RT_RECT_YZ = 2 };
 int rt_abi_version(void);
 const char* rt_last_error(void);
 int rt_device_count(int* out_count);
-/* Context on one HIP device; owns a HIP stream and all device memory. */
+/* Context on one HIP device; owns a HIP stream and all device memory.
+ * The render lanes' path pools belong to the context and are shared by every
+ * scene rendered on it.  They are sized at the context's first render to
+ * hold up to 288M paths, but at most 55 % of the device memory free at that
+ * moment (RTAMD_MAX_PATHS overrides), and are kept for later renders;
+ * rt_context_release_pools frees them (the next render sizes them again),
+ * e.g. before the caller allocates large buffers of its own. */
 int rt_context_create(int device, int* out_ctx);
 int rt_context_destroy(int ctx);
+int rt_context_release_pools(int ctx);
 
 /* ---- scene building (replaces the closure-vector constructors) ---------- */
 int rt_scene_begin(int ctx, int* out_scene);
@@ -179,6 +186,15 @@ int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* 
  * rt_last_error() naming them ("device fault (flags N): ..."). */
 enum { RT_FAULT_REJECT = 1, RT_FAULT_CURVE = 2, RT_FAULT_PATH = 4, RT_FAULT_SHARD = 8, RT_FAULT_LDS = 16 };
 
+/* The world's closest hit for n rays (hit-obj-list over the scene list,
+ * geometry.scm:33-50, with t in (0.001, 999999999999) as color asks it,
+ * main.scm:104): rays = n x {ox, oy, oz, dx, dy, dz, time} (host memory);
+ * out_t[i] = the hit's t and out_mat[i] = its material id (rt_add_material_*),
+ * or out_mat[i] = -1 (and t 0) for a miss.  A diagnostic and test probe (the
+ * oracle's orc_hit_world); scenes with constant media are refused, since the
+ * medium's hit test draws from the path's random stream. */
+int rt_hit_rays(int scene, int n, const double* rays, double* out_t, int32_t* out_mat);
+
 /* Statistics of the last render on this scene. */
 typedef struct rt_stats {
     uint64_t segments;    /* closest-hit queries issued by the integrator (ray segments) */
@@ -197,6 +213,8 @@ typedef struct rt_stats {
     uint64_t shade_survivors; /* paths the shade kernels wrote on to the next iteration */
     uint32_t chunks;          /* sample chunks the render was cut into (path pools) */
     uint32_t lanes;           /* render lanes (path pool + stream) kept in flight */
+    uint64_t curve_pooled_batches; /* curve subdivision passes over a full survivor pool (wavefront curve kernels) */
+    uint64_t curve_flat_pooled;    /* curves those passes walked whose root is a leaf (flat: depth estimate < 0) */
 } rt_stats;
 int rt_get_stats(int scene, rt_stats* out);
 

@@ -86,6 +86,9 @@ def lib():
             "orc_tex_value": ([V, ctypes.c_int, _dp, _dp], None),
             "orc_onb": ([_dp, _dp], None),
             "orc_hit_world": ([V, _dp, _dp, ctypes.c_double, _dp], ctypes.c_int),
+            "orc_set_bvh_flat": ([V, ctypes.c_int], None),
+            "orc_trace_sample": ([V, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                  ctypes.c_uint32, _dp, ctypes.c_int], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -188,6 +191,10 @@ class OracleScene:
     def light_pdf_value(self, o, v):
         return self.L.orc_light_pdf_value(self.s, _dv(o), _dv(v))
 
+    def set_bvh_flat(self, flat):
+        """True: evaluate every BVH as the flat list it restates (no tree)."""
+        self.L.orc_set_bvh_flat(self.s, 1 if flat else 0)
+
     def set_sky(self, code):
         self.L.orc_set_sky(self.s, code)
 
@@ -218,6 +225,12 @@ class OracleScene:
         out = (ctypes.c_double * 3)()
         self.L.orc_sample(self.s, nx, ny, x, y, seed, smp, out)
         return tuple(out)
+
+    def trace_sample(self, nx, ny, x, y, seed, smp, cap=128):
+        """Debugging aid: the sample's path as rows (o3, d3, hit, t, p3, mat, draw counter)."""
+        out = np.zeros(13 * cap)
+        n = self.L.orc_trace_sample(self.s, nx, ny, x, y, seed, smp, out.ctypes.data_as(_dp), cap)
+        return out[:13 * n].reshape(n, 13)
 
     def hit_world(self, o, d, time=0.0):
         out = (ctypes.c_double * 8)()

@@ -129,6 +129,18 @@ typedef struct {
     double density;                     /* OBJ_MEDIUM (child = boundary, mat = phase lambertian) */
 } orc_obj;
 
+/* A conservative f64 bounding-volume tree over one OBJ_BVH's primitives (see
+ * "BVH" below).  Leaves hold up to 4 primitives of prim[]; node boxes are
+ * padded outward, so culling never removes a primitive that could win. */
+typedef struct { double lo[3], hi[3]; int left, right, first, count; } orc_bnode;
+typedef struct {
+    int nprim;
+    int* prim;                          /* object ids, in leaf order */
+    int* order;                         /* each one's index in the flattened list (tie-breaks) */
+    unsigned char* nonstrict;           /* 1: hits at t == t-max (curves), 0: only t < t-max (spheres) */
+    orc_bnode* node; int nnode, cnode;
+} orc_bvh;
+
 typedef struct {
     orc_tex* tex; int ntex, ctex;
     orc_mat* mat; int nmat, cmat;
@@ -140,6 +152,10 @@ typedef struct {
     v3 ranvec[256];
     int perm_x[256], perm_y[256], perm_z[256];
     int have_perlin;
+    /* OBJ_BVH acceleration (built lazily by scene_prepare; bvh_of[obj] = -1: flat list) */
+    orc_bvh* bvh; int nbvh;
+    int* bvh_of; int nbvh_of;
+    int bvh_ready, bvh_flat;
 } orc_scene;
 
 #define GROW(ptr, n, cap)                                                    \
@@ -156,8 +172,16 @@ orc_scene* orc_scene_new(void) {
     s->light = -1;
     return s;
 }
+static void bvh_clear(orc_scene* s) {
+    for (int i = 0; i < s->nbvh; ++i) {
+        free(s->bvh[i].prim); free(s->bvh[i].order); free(s->bvh[i].nonstrict); free(s->bvh[i].node);
+    }
+    free(s->bvh); free(s->bvh_of);
+    s->bvh = 0; s->nbvh = 0; s->bvh_of = 0; s->nbvh_of = 0; s->bvh_ready = 0;
+}
 void orc_scene_free(orc_scene* s) {
     if (!s) return;
+    bvh_clear(s);
     free(s->tex); free(s->mat); free(s->obj); free(s->kids); free(s);
 }
 
@@ -192,6 +216,7 @@ int orc_add_material_dielectric(orc_scene* s, double ref) { return add_mat(s, MA
 int orc_add_material_diffuse_light(orc_scene* s, int tex) { return add_mat(s, MAT_DIFFUSE_LIGHT, tex, 0, 0); }
 
 static int new_obj(orc_scene* s, int type) {
+    s->bvh_ready = 0;
     GROW(s->obj, s->nobj, s->cobj);
     memset(&s->obj[s->nobj], 0, sizeof(orc_obj));
     s->obj[s->nobj].type = type;
@@ -293,7 +318,10 @@ int orc_add_bezier_array(orc_scene* s, const double* cps, int n, double width, i
     return first;
 }
 
-void orc_set_camera(orc_scene* s, const double cam[24]) { memcpy(s->cam, cam, sizeof s->cam); }
+void orc_set_camera(orc_scene* s, const double cam[24]) { memcpy(s->cam, cam, sizeof s->cam); s->bvh_ready = 0; }
+/* 1: traverse every OBJ_BVH as the flat list it restates (the tie-break
+ * semantics the trees reproduce); 0 (default): use the trees. */
+void orc_set_bvh_flat(orc_scene* s, int flat) { s->bvh_flat = flat; }
 void orc_set_sky(orc_scene* s, int sky) { s->sky = sky; }
 void orc_set_light_sampling(orc_scene* s, int obj) { s->light = obj; }
 void orc_set_world(orc_scene* s, int world) { s->world = world; }
@@ -679,6 +707,330 @@ static int rect_hit(const orc_obj* o, ray_t r, double tmin, double tmax, hitrec*
     return 1;
 }
 
+/* ------------------------------------------------------------------ BVH
+ * geometry.scm:226-260 (make-bvh-node) and :294-371 (make-bvh-with-sah) build
+ * trees whose hit visits both children with the same t-max and keeps the
+ * closer record; their closest hit does not depend on the tree's shape (SURVEY
+ * App. A Q13-Q15).  The oracle restates an OBJ_BVH as the closest-hit list of
+ * its objects (hit-obj-list, geometry.scm:33-50) and, so that a 2^20-curve
+ * scene (C5) can be checked at all, evaluates that list through a
+ * conservative f64 tree whose result is the list's, tie-breaks included:
+ *  - nested lists flatten exactly: a list scanned with the running closest t
+ *    is the same scan as its elements spliced in;
+ *  - a sphere / moving sphere / curve has a candidate t that does not depend
+ *    on the t-max it is asked with, only whether it is reported: spheres
+ *    report t < t-max (geometry.scm:157,165), curves t <= t-max (bezier.scm:164
+ *    rejects only `(< t (v:z p))`; converge's cull :126 never removes a leaf
+ *    hit, which lies in every ancestor's hull);
+ *  - a list scan therefore returns the element with the smallest t; among the
+ *    elements tied there, the first in list order, unless a later tied one
+ *    reports at t == t-max (a curve), in which case the last such.  The
+ *    incoming t-max acts as a virtual first element at that t.
+ * Trees are built only over lists of spheres, moving spheres and curves (a
+ * rect can report t = NaN, Q20, which no tree can order); anything else stays
+ * a flat list.  Boxes: sphere c +- |r|; moving sphere the union over the ray
+ * times that occur (the camera shutter and 0, Q4); curve = control points +-
+ * width/2 (a curve hit lies within width/2 of its hull, bezier.scm:88-98,
+ * 159-166).  Every box is padded by 1e-6 x the scene's coordinate bound, far
+ * above the rounding of the hit tests (the worst, a near-tangent sphere root,
+ * is off by ~3e-8 x the origin distance), so culling is conservative. */
+typedef struct { double lo[3], hi[3], c[3]; int obj, order; unsigned char ns; } orc_bprim;
+
+static int bvh_flatten(const orc_scene* s, int id, int** out, int* n, int* cap) {
+    const orc_obj* o = &s->obj[id];
+    if (o->type == OBJ_LIST || o->type == OBJ_BVH) {
+        for (int j = 0; j < o->count; ++j)
+            if (!bvh_flatten(s, s->kids[o->first + j], out, n, cap)) return 0;
+        return 1;
+    }
+    if (o->type != OBJ_SPHERE && o->type != OBJ_MOVING_SPHERE && o->type != OBJ_BEZIER) return 0;
+    GROW(*out, *n, *cap);
+    (*out)[(*n)++] = id;
+    return 1;
+}
+
+static double fin_abs(double x) { return isfinite(x) ? fabs(x) : 0.0; }
+
+static double sa_of(const double lo[3], const double hi[3]) {
+    double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    double a = 2 * (dx * dy + dx * dz + dy * dz);
+    return isfinite(a) ? a : 1e300;
+}
+
+static int bvh_new_node(orc_bvh* B) {
+    GROW(B->node, B->nnode, B->cnode);
+    memset(&B->node[B->nnode], 0, sizeof(orc_bnode));
+    return B->nnode++;
+}
+
+static int cmp_axis;
+static int cmp_centroid(const void* a, const void* b) {
+    double x = ((const orc_bprim*)a)->c[cmp_axis], y = ((const orc_bprim*)b)->c[cmp_axis];
+    return (x < y) ? -1 : (x > y) ? 1 : 0;
+}
+
+static int bvh_build(orc_bvh* B, orc_bprim* P, int lo, int hi, int depth) {
+    int id = bvh_new_node(B);
+    double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = lo; i < hi; ++i)
+        for (int a = 0; a < 3; ++a) {
+            if (P[i].lo[a] < blo[a]) blo[a] = P[i].lo[a];
+            if (P[i].hi[a] > bhi[a]) bhi[a] = P[i].hi[a];
+            if (P[i].c[a] < clo[a]) clo[a] = P[i].c[a];
+            if (P[i].c[a] > chi[a]) chi[a] = P[i].c[a];
+        }
+    memcpy(B->node[id].lo, blo, sizeof blo);
+    memcpy(B->node[id].hi, bhi, sizeof bhi);
+    int n = hi - lo;
+    if (n <= 4) {
+        B->node[id].first = lo; B->node[id].count = n; B->node[id].left = B->node[id].right = -1;
+        return id;
+    }
+    /* binned SAH over centroids (16 bins per axis); median split as the fallback */
+    enum { NB = 16 };
+    int best_axis = -1, best_bin = -1;
+    double best_cost = INFINITY;
+    for (int a = 0; a < 3 && depth < 64; ++a) {
+        double ext = chi[a] - clo[a];
+        if (!(ext > 0) || !isfinite(ext)) continue;
+        int cnt[NB] = {0};
+        double bl[NB][3], bh[NB][3];
+        for (int k = 0; k < NB; ++k)
+            for (int q = 0; q < 3; ++q) { bl[k][q] = INFINITY; bh[k][q] = -INFINITY; }
+        for (int i = lo; i < hi; ++i) {
+            int k = (int)((P[i].c[a] - clo[a]) / ext * NB);
+            k = k < 0 ? 0 : (k >= NB ? NB - 1 : k);
+            cnt[k]++;
+            for (int q = 0; q < 3; ++q) {
+                if (P[i].lo[q] < bl[k][q]) bl[k][q] = P[i].lo[q];
+                if (P[i].hi[q] > bh[k][q]) bh[k][q] = P[i].hi[q];
+            }
+        }
+        double rsa[NB]; int rcnt[NB];
+        double rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int rc = 0;
+        for (int k = NB - 1; k > 0; --k) {
+            rc += cnt[k];
+            for (int q = 0; q < 3; ++q) {
+                if (bl[k][q] < rl[q]) rl[q] = bl[k][q];
+                if (bh[k][q] > rh[q]) rh[q] = bh[k][q];
+            }
+            rsa[k] = rc ? sa_of(rl, rh) : 0; rcnt[k] = rc;
+        }
+        double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int lc = 0;
+        for (int k = 0; k < NB - 1; ++k) {
+            lc += cnt[k];
+            for (int q = 0; q < 3; ++q) {
+                if (bl[k][q] < ll[q]) ll[q] = bl[k][q];
+                if (bh[k][q] > lh[q]) lh[q] = bh[k][q];
+            }
+            if (!lc || !rcnt[k + 1]) continue;
+            double cost = sa_of(ll, lh) * lc + rsa[k + 1] * rcnt[k + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = k; }
+        }
+    }
+    int mid;
+    if (best_axis >= 0) {
+        const int a = best_axis;
+        const double ext = chi[a] - clo[a];
+        int i = lo, j = hi - 1;
+        while (i <= j) {
+            int k = (int)((P[i].c[a] - clo[a]) / ext * NB);
+            k = k < 0 ? 0 : (k >= NB ? NB - 1 : k);
+            if (k <= best_bin) { ++i; } else { orc_bprim t = P[i]; P[i] = P[j]; P[j] = t; --j; }
+        }
+        mid = i;
+    } else {
+        mid = lo;
+    }
+    if (mid <= lo || mid >= hi) {            /* no usable SAH split: median on the widest centroid axis */
+        int a = 0;
+        double w = -1;
+        for (int q = 0; q < 3; ++q) {
+            double e = chi[q] - clo[q];
+            if (isfinite(e) && e > w) { w = e; a = q; }
+        }
+        cmp_axis = a;
+        qsort(P + lo, (size_t)n, sizeof(orc_bprim), cmp_centroid);
+        mid = lo + n / 2;
+    }
+    int l = bvh_build(B, P, lo, mid, depth + 1);
+    int r = bvh_build(B, P, mid, hi, depth + 1);
+    B->node[id].left = l; B->node[id].right = r; B->node[id].count = 0;
+    return id;
+}
+
+/* Build every OBJ_BVH's tree (idempotent until the scene or camera changes). */
+static void scene_prepare(orc_scene* s) {
+    if (s->bvh_ready) return;
+    bvh_clear(s);
+    s->bvh_of = malloc(sizeof(int) * (size_t)(s->nobj ? s->nobj : 1));
+    s->nbvh_of = s->nobj;
+    for (int i = 0; i < s->nobj; ++i) s->bvh_of[i] = -1;
+    /* coordinate bound of the scene: every ray origin and hit point lies within it */
+    double R = fin_abs(s->cam[9]) + fin_abs(s->cam[10]) + fin_abs(s->cam[11]) + fin_abs(s->cam[21]);
+    for (int i = 0; i < s->nobj; ++i) {
+        const orc_obj* o = &s->obj[i];
+        double m = 0, t = 0;
+        switch (o->type) {
+        case OBJ_SPHERE: m = fmax(fmax(fin_abs(o->c0.x), fin_abs(o->c0.y)), fin_abs(o->c0.z)) + fin_abs(o->r); break;
+        case OBJ_MOVING_SPHERE:
+            m = fmax(fmax(fmax(fin_abs(o->c0.x), fin_abs(o->c0.y)), fmax(fin_abs(o->c0.z), fin_abs(o->c1.x))),
+                     fmax(fin_abs(o->c1.y), fin_abs(o->c1.z))) + fin_abs(o->r);
+            break;
+        case OBJ_RECT: m = fmax(fmax(fmax(fin_abs(o->a0), fin_abs(o->a1)), fmax(fin_abs(o->b0), fin_abs(o->b1))),
+                                fin_abs(o->k)); break;
+        case OBJ_BOX: m = fmax(fmax(fmax(fin_abs(o->c0.x), fin_abs(o->c0.y)), fin_abs(o->c0.z)),
+                               fmax(fmax(fin_abs(o->c1.x), fin_abs(o->c1.y)), fin_abs(o->c1.z))); break;
+        case OBJ_TRANSLATE: t = fin_abs(o->c0.x) + fin_abs(o->c0.y) + fin_abs(o->c0.z); break;
+        case OBJ_BEZIER:
+            for (int k = 0; k < 4; ++k)
+                m = fmax(m, fmax(fmax(fin_abs(o->cp[k].x), fin_abs(o->cp[k].y)), fin_abs(o->cp[k].z)));
+            m += fin_abs(o->width);
+            break;
+        default: break;
+        }
+        if (m > R) R = m;
+        R += t;                               /* instance offsets move geometry outward */
+    }
+    const double pad = 1e-6 * fmax(R, 1e4);
+    double tlo = 0, thi = 0;                  /* ray times: the shutter and 0 */
+    if (isfinite(s->cam[22])) { tlo = fmin(tlo, s->cam[22]); thi = fmax(thi, s->cam[22]); }
+    if (isfinite(s->cam[23])) { tlo = fmin(tlo, s->cam[23]); thi = fmax(thi, s->cam[23]); }
+    int* ids = 0; int cap = 0;
+    for (int i = 0; i < s->nobj; ++i) {
+        if (s->obj[i].type != OBJ_BVH) continue;
+        int n = 0;
+        if (!bvh_flatten(s, i, &ids, &n, &cap) || n < 8) continue;
+        orc_bprim* P = malloc(sizeof(orc_bprim) * (size_t)n);
+        for (int j = 0; j < n; ++j) {
+            const orc_obj* o = &s->obj[ids[j]];
+            double lo[3], hi[3];
+            if (o->type == OBJ_SPHERE) {
+                double c[3] = {o->c0.x, o->c0.y, o->c0.z}, rr = fabs(o->r);
+                for (int a = 0; a < 3; ++a) { lo[a] = c[a] - rr; hi[a] = c[a] + rr; }
+            } else if (o->type == OBJ_MOVING_SPHERE) {
+                double rr = fabs(o->r);
+                double ts[2] = {tlo, thi};
+                for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+                for (int k = 0; k < 2; ++k) {
+                    v3 c = vadd(o->c0, vscale(vsub(o->c1, o->c0), (ts[k] - o->t0) / (o->t1 - o->t0)));
+                    double cc[3] = {c.x, c.y, c.z};
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = fmin(lo[a], cc[a] - rr); hi[a] = fmax(hi[a], cc[a] + rr);
+                    }
+                }
+            } else {
+                double w = fabs(o->width) / 2;
+                for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+                for (int k = 0; k < 4; ++k) {
+                    double cc[3] = {o->cp[k].x, o->cp[k].y, o->cp[k].z};
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = fmin(lo[a], cc[a] - w); hi[a] = fmax(hi[a], cc[a] + w);
+                    }
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                if (!isfinite(lo[a]) || !isfinite(hi[a])) { lo[a] = -INFINITY; hi[a] = INFINITY; }
+                else { lo[a] -= pad; hi[a] += pad; }
+                P[j].lo[a] = lo[a]; P[j].hi[a] = hi[a];
+                P[j].c[a] = isfinite(lo[a]) ? 0.5 * (lo[a] + hi[a]) : 0.0;
+            }
+            P[j].obj = ids[j]; P[j].order = j; P[j].ns = (o->type == OBJ_BEZIER);
+        }
+        s->bvh = realloc(s->bvh, sizeof(orc_bvh) * (size_t)(s->nbvh + 1));
+        orc_bvh* B = &s->bvh[s->nbvh];
+        memset(B, 0, sizeof *B);
+        bvh_build(B, P, 0, n, 0);
+        B->nprim = n;
+        B->prim = malloc(sizeof(int) * (size_t)n);
+        B->order = malloc(sizeof(int) * (size_t)n);
+        B->nonstrict = malloc((size_t)n);
+        for (int j = 0; j < n; ++j) { B->prim[j] = P[j].obj; B->order[j] = P[j].order; B->nonstrict[j] = P[j].ns; }
+        free(P);
+        s->bvh_of[i] = s->nbvh++;
+    }
+    free(ids);
+    s->bvh_ready = 1;
+}
+
+/* Slab test of a padded box against [0, cut] along the raw ray (geometry.scm:
+ * 73-105 tests each axis against the original interval; intersecting the axes
+ * as done here only culls more, and only boxes the ray cannot reach). */
+static int bvh_slab(const orc_bnode* nd, const double o[3], const double d[3], const double inv[3], double cut,
+                    double* tnear) {
+    double t0 = -INFINITY, t1 = INFINITY;
+    for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0) {
+            if (o[a] < nd->lo[a] || o[a] > nd->hi[a]) return 0;
+            continue;
+        }
+        double ta = (nd->lo[a] - o[a]) * inv[a], tb = (nd->hi[a] - o[a]) * inv[a];
+        if (ta > tb) { double t = ta; ta = tb; tb = t; }
+        if (ta > t0) t0 = ta;
+        if (tb < t1) t1 = tb;
+    }
+    if (t0 > t1 || t1 < 0 || t0 > cut) return 0;
+    *tnear = t0;
+    return 1;
+}
+
+static int prim_hit(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec);
+
+static int bvh_hit(const orc_scene* s, const orc_bvh* B, const orc_obj* flat, ray_t r, double tmin, double tmax,
+                   hitrec* rec) {
+    const double dl = vlength(r.d);
+    /* a curve reports distance along unit(dir) (Q10): raw parameter = t / |dir| */
+    const double scale = (dl < 1) ? 1 / dl : 1;
+    if (!(scale < INFINITY) || B->nnode == 0) return hit_list(s, flat->first, flat->count, r, tmin, tmax, rec);
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
+    double best = tmax;
+    int first = -1, ns = -1, first_ns = 0;   /* first = -1: the virtual element at t-max */
+    hitrec first_rec, ns_rec, h;
+    int stack[256], sp = 0;
+    double tn;
+    if (!bvh_slab(&B->node[0], o, d, inv, best * scale * (1 + 1e-12), &tn)) return 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const orc_bnode* nd = &B->node[stack[--sp]];
+        const double cut = best * scale * (1 + 1e-12);
+        if (nd->count) {
+            for (int k = nd->first; k < nd->first + nd->count; ++k) {
+                if (!prim_hit(s, B->prim[k], r, tmin, nextafter(best, INFINITY), &h)) continue;
+                const int idx = B->order[k], hns = B->nonstrict[k];
+                if (h.t < best) {
+                    best = h.t; first = idx; first_rec = h; first_ns = hns; ns = -1;
+                } else if (h.t == best) {
+                    if (idx < first) {                  /* the displaced first is a later tied element */
+                        if (first_ns && first >= 0 && first > ns) { ns = first; ns_rec = first_rec; }
+                        first = idx; first_rec = h; first_ns = hns;
+                    } else if (hns && idx > ns) {
+                        ns = idx; ns_rec = h;
+                    }
+                }
+            }
+            continue;
+        }
+        double tl, tr;
+        int hl = bvh_slab(&B->node[nd->left], o, d, inv, cut, &tl);
+        int hr = bvh_slab(&B->node[nd->right], o, d, inv, cut, &tr);
+        if (hl && hr) {
+            if (tl <= tr) { stack[sp++] = nd->right; stack[sp++] = nd->left; }
+            else { stack[sp++] = nd->left; stack[sp++] = nd->right; }
+        } else if (hl) {
+            stack[sp++] = nd->left;
+        } else if (hr) {
+            stack[sp++] = nd->right;
+        }
+    }
+    if (ns >= 0 && ns > first) { *rec = ns_rec; return 1; }
+    if (first >= 0) { *rec = first_rec; return 1; }
+    return 0;
+}
+
 static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec) {
     const orc_obj* o = &s->obj[id];
     switch (o->type) {
@@ -715,7 +1067,10 @@ static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax
         return 1;
     }
     case OBJ_LIST:
+        return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
     case OBJ_BVH:
+        if (!s->bvh_flat && id < s->nbvh_of && s->bvh_of[id] >= 0)
+            return bvh_hit(s, &s->bvh[s->bvh_of[id]], o, r, tmin, tmax, rec);
         return hit_list(s, o->first, o->count, r, tmin, tmax, rec);
     case OBJ_BEZIER:
         return bezier_hit(o, r, tmin, tmax, rec);
@@ -743,6 +1098,10 @@ static int hit_obj(const orc_scene* s, int id, ray_t r, double tmin, double tmax
     }
     }
     return 0;
+}
+
+static int prim_hit(const orc_scene* s, int id, ray_t r, double tmin, double tmax, hitrec* rec) {
+    return hit_obj(s, id, r, tmin, tmax, rec);
 }
 
 /* ---------------------------------------------------------- material.scm */
@@ -789,6 +1148,7 @@ void orc_onb(const double n[3], double out[9]) {
 }
 /* closest hit of the world list: returns 1 on hit, rec = {t, p(3), n(3), mat} */
 int orc_hit_world(const orc_scene* s, const double o[3], const double d[3], double time, double out[8]) {
+    scene_prepare((orc_scene*)s);
     ray_t r = {V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), time};
     hitrec rec;
     const orc_obj* w = &s->obj[s->world];
@@ -875,6 +1235,10 @@ double orc_light_pdf_value(const orc_scene* s, const double o[3], const double v
 typedef struct { uint64_t segments; int max_depth; } orc_counters;
 
 /* main.scm:100-121 — recursive colour */
+/* debugging aid (orc_trace_sample): per segment o, d, hit?, t, p, mat, draw counter */
+static __thread double* tl_trace;
+static __thread int tl_trace_n, tl_trace_cap;
+
 static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters* cnt) {
     hitrec rec;
     const orc_obj* w = &s->obj[s->world];
@@ -883,6 +1247,12 @@ static v3 color(const orc_scene* s, ray_t r, int depth, orc_rng* g, orc_counters
     tl_rng = g;
     int hit = hit_list(s, w->first, w->count, r, ORC_TMIN, ORC_TMAX, &rec);
     tl_rng = 0;
+    if (tl_trace && tl_trace_n < tl_trace_cap) {
+        double* q = tl_trace + 13 * tl_trace_n++;
+        q[0] = r.o.x; q[1] = r.o.y; q[2] = r.o.z; q[3] = r.d.x; q[4] = r.d.y; q[5] = r.d.z;
+        q[6] = hit; q[7] = hit ? rec.t : 0; q[8] = hit ? rec.p.x : 0; q[9] = hit ? rec.p.y : 0;
+        q[10] = hit ? rec.p.z : 0; q[11] = hit ? rec.mat : -1; q[12] = g->ctr;
+    }
     if (!hit) return sky(s, r);
     const orc_mat* m = &s->mat[rec.mat];
     switch (m->type) {
@@ -999,6 +1369,7 @@ static v3 sample_pixel(const orc_scene* s, int nx, int ny, int x, int y, uint64_
 
 void orc_sample(const orc_scene* s, int nx, int ny, int x, int y, uint64_t seed, uint32_t smp,
                 double out[3]) {
+    scene_prepare((orc_scene*)s);
     orc_counters cnt = {0, 0};
     v3 c = sample_pixel(s, nx, ny, x, y, seed, smp, &cnt);
     out[0] = c.x; out[1] = c.y; out[2] = c.z;
@@ -1012,6 +1383,7 @@ void orc_sample(const orc_scene* s, int nx, int ny, int x, int y, uint64_t seed,
 uint64_t orc_render(const orc_scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
                     double* accum, long pix_begin, long pix_end, int nthreads) {
     uint64_t total = 0;
+    scene_prepare((orc_scene*)s);
     if (pix_end < 0 || pix_end > (long)nx * ny) pix_end = (long)nx * ny;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
@@ -1035,6 +1407,7 @@ uint64_t orc_render(const orc_scene* s, int nx, int ny, int spp_begin, int spp_c
 uint64_t orc_render_pixels(const orc_scene* s, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
                            double* accum, const uint32_t* pix, long npix, int nthreads) {
     uint64_t total = 0;
+    scene_prepare((orc_scene*)s);
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : total)
 #endif
@@ -1052,6 +1425,17 @@ uint64_t orc_render_pixels(const orc_scene* s, int nx, int ny, int spp_begin, in
     }
     (void)nthreads;
     return total;
+}
+
+/* debugging aid: one sample's path, 13 doubles per segment (see color()); returns the segment count */
+int orc_trace_sample(const orc_scene* s, int nx, int ny, int x, int y, uint64_t seed, uint32_t smp, double* out,
+                     int cap) {
+    scene_prepare((orc_scene*)s);
+    orc_counters cnt = {0, 0};
+    tl_trace = out; tl_trace_n = 0; tl_trace_cap = cap;
+    (void)sample_pixel(s, nx, ny, x, y, seed, smp, &cnt);
+    tl_trace = 0;
+    return tl_trace_n;
 }
 
 /* exported KAT helper: util.scm:37-44 with given (r1, r2) */

@@ -38,6 +38,8 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
                              const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
+hipError_t take_curve_stats(unsigned long long out[2]);
+hipError_t launch_hit_rays(const DevScene&, const double*, uint32_t, double*, int32_t*, hipStream_t);
 hipError_t set_reject_cap(int);
 }  // namespace rtamd
 
@@ -93,11 +95,6 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-struct Context {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    DevBuf accum_tmp, img_tmp;
-};
 
 // A lane = one path pool + stream.  render_impl deals the sample chunks of a
 // render to the lanes round-robin and keeps them in flight together, so the
@@ -131,9 +128,19 @@ struct Lane {
     }
 };
 
+// A context owns the render lanes' path pools: every scene rendered on it
+// shares them (the C ABI renders one scene at a time per context), so a
+// second scene does not take a second 55 % of device memory.
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf accum_tmp, img_tmp;
+    size_t pool_cap = 0;                       // paths per chunk (max_paths), fixed at the first render
+    std::unique_ptr<Lane> lanes[kLanes];       // rt_context_release_pools frees them
+};
+
 struct Scene {
     int ctx = -1;
-    size_t pool_cap = 0;                       // paths per chunk (max_paths), fixed at the first render
     std::vector<DevTexture> texs;
     std::vector<DevMaterial> mats;
     std::vector<Obj> objs;
@@ -156,9 +163,8 @@ struct Scene {
     uint32_t ext_lds_blocks = 0;
     size_t cam_lds = 0;                            // k_camera (fused raygen + depth-0 extend), same
     uint32_t cam_blocks = 0;
-    // render buffers: one path pool per lane (render_impl)
+    // render buffers (the lanes' path pools belong to the context)
     DevBuf pixlist;
-    std::unique_ptr<Lane> lanes[kLanes];
     int pix_nx = -1, pix_ny = -1, pix_y0 = -1, pix_y1 = -1, pix_shard = -1, pix_nshard = -1;
     uint32_t pix_n = 0;
     bool profiling = false;
@@ -299,7 +305,7 @@ struct BvhBuild {
     std::vector<BvhNode> nodes;
     int leaf_max = 2;                 // RTAMD_BVH_LEAF
     bool singles = false;             // split down to one primitive per leaf even where SAH would stop
-    double trav_cost = 0.5;           // RTAMD_BVH_CT: node visit cost relative to one primitive test
+    double trav_cost = 0.5;           // node visit cost relative to one primitive test
     int sweep_max = 0;                // RTAMD_BVH_SWEEP: nodes of at most this many primitives use the exact SAH sweep
     static constexpr int kBins = 16;
 
@@ -307,6 +313,12 @@ struct BvhBuild {
         const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
         if (dx < 0 || dy < 0 || dz < 0) return 0.0;
         return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+    // centroid order with NaN last (a degenerate shutter can give NaN boxes): a strict
+    // weak ordering, which std::stable_sort / nth_element require
+    static bool c_less(const double x, const double y) {
+        if (std::isnan(x)) return false;
+        return std::isnan(y) || x < y;
     }
     static void grow(double* lo, double* hi, const double* plo, const double* phi) {
         for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], plo[k]); hi[k] = std::max(hi[k], phi[k]); }
@@ -332,7 +344,7 @@ struct BvhBuild {
             std::vector<double> right(n + 1);
             for (int ax = 0; ax < 3; ++ax) {
                 for (int i = 0; i < n; ++i) ord[i] = b + i;
-                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return refs[x].c[ax] < refs[y].c[ax]; });
+                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return c_less(refs[x].c[ax], refs[y].c[ax]); });
                 double rlo[3] = {1e300, 1e300, 1e300}, rhi[3] = {-1e300, -1e300, -1e300};
                 for (int i = n - 1; i >= 1; --i) { grow(rlo, rhi, refs[ord[i]].lo, refs[ord[i]].hi); right[i] = area(rlo, rhi); }
                 double llo[3] = {1e300, 1e300, 1e300}, lhi[3] = {-1e300, -1e300, -1e300};
@@ -348,7 +360,7 @@ struct BvhBuild {
                 const bool worth = parent <= 0 || trav_cost + best / parent < (double)n;
                 if (!worth && n <= 2 * leaf_max && !singles) return make_leaf(node, b, e, lo, hi);
                 std::stable_sort(refs.begin() + b, refs.begin() + e,
-                                 [&](const PrimRef& x, const PrimRef& y) { return x.c[best_axis] < y.c[best_axis]; });
+                                 [&](const PrimRef& x, const PrimRef& y) { return c_less(x.c[best_axis], y.c[best_axis]); });
                 const int l = build(b, b + best_i, depth + 1);
                 const int r = build(b + best_i, e, depth + 1);
                 BvhNode& N = nodes[node];
@@ -366,8 +378,9 @@ struct BvhBuild {
             double blo[kBins][3], bhi[kBins][3];
             for (int k = 0; k < kBins; ++k) for (int j = 0; j < 3; ++j) { blo[k][j] = 1e300; bhi[k][j] = -1e300; }
             auto bin_of = [&](const PrimRef& r) {
-                int k = (int)((r.c[axis] - clo[axis]) / ext * kBins);
-                return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+                const double f = (r.c[axis] - clo[axis]) / ext * kBins;
+                if (!(f >= 0.0)) return 0;                      // NaN centroids go to the first bin
+                return f >= (double)kBins ? kBins - 1 : (int)f;
             };
             for (int i = b; i < e; ++i) { const int k = bin_of(refs[i]); cnt[k]++; grow(blo[k], bhi[k], refs[i].lo, refs[i].hi); }
             double best = 1e300;
@@ -394,7 +407,7 @@ struct BvhBuild {
         if (mid <= b || mid >= e) {                  // degenerate: median split on the axis
             mid = b + n / 2;
             std::nth_element(refs.begin() + b, refs.begin() + mid, refs.begin() + e,
-                             [&](const PrimRef& x, const PrimRef& y) { return x.c[axis] < y.c[axis]; });
+                             [&](const PrimRef& x, const PrimRef& y) { return c_less(x.c[axis], y.c[axis]); });
         }
         const int l = build(b, mid, depth + 1);
         const int r = build(mid, e, depth + 1);
@@ -518,10 +531,7 @@ void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_
     for (int dd : depth) lane_stack = std::max(lane_stack, dd);
 }
 
-size_t extend_lds_budget() {     // RTAMD_EXTEND_LDS_MAX: largest LDS footprint k_extend_lds may take
-    const char* e = std::getenv("RTAMD_EXTEND_LDS_MAX");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)64 << 10;
-}
+size_t extend_lds_budget() { return (size_t)64 << 10; }   // largest LDS footprint k_extend_lds may take
 
 int commit_scene(Scene* s, int world) {
     Context* c = get_ctx(s->ctx);
@@ -629,7 +639,6 @@ int commit_scene(Scene* s, int world) {
         bb.leaf_max = std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; })
                           ? 2 : 1;
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("RTAMD_BVH_CT")) bb.trav_cost = std::atof(e);
         bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
                                      std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));
         bb.build(0, (int)refs.size(), 0);
@@ -940,7 +949,7 @@ int commit_scene(Scene* s, int world) {
     d.n_sph = (int)sph.size(); d.n_msph = (int)msph.size(); d.n_rect = (int)rect.size();
     d.n_groups = (int)groups.size(); d.n_chains = (int)chains.size(); d.n_leaves = (int)leaves.size();
     d.msph_shared = 0;
-    if (!msph.empty() && !std::getenv("RTAMD_NO_MSPH_SHARED")) {
+    if (!msph.empty()) {
         bool same = true;
         for (const MSphereRec& m : msph)
             same = same && std::memcmp(&m.t0, &msph[0].t0, sizeof(double)) == 0 &&
@@ -1021,20 +1030,11 @@ PixSel full_frame(int ny) { return PixSel{0, ny, 0, 1}; }
 std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
     const int T = 16;
     const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
-    static const bool quad = std::getenv("RTAMD_PIX_QUAD") != nullptr;   // A/B: 8x8 quads per wave
     std::vector<uint32_t> out;
     out.reserve((size_t)nx * (size_t)(ps.y1 - ps.y0) / (size_t)ps.nshard + T * T);
     for (int t = 0; t < tx * ty; ++t) {
         if (t % ps.nshard != ps.shard) continue;
         const int bx = (t % tx) * T, by = (t / tx) * T;
-        if (quad && bx + T <= nx && by + T <= ny && by >= ps.y0 && by + T <= ps.y1) {
-            // a whole tile: its four 8x8 quads in turn, so a wave's 64 pixels are a square
-            for (int q = 0; q < 4; ++q)
-                for (int yy = by + (q >> 1) * 8; yy < by + (q >> 1) * 8 + 8; ++yy)
-                    for (int xx = bx + (q & 1) * 8; xx < bx + (q & 1) * 8 + 8; ++xx)
-                        out.push_back((uint32_t)(yy * nx + xx));
-            continue;
-        }
         for (int yy = std::max(by, ps.y0); yy < std::min(std::min(by + T, ny), ps.y1); ++yy)
             for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
     }
@@ -1044,7 +1044,7 @@ std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
 std::string fault_text(uint32_t f) {
     std::string m = "device fault (flags " + std::to_string(f) + "):";
     if (f & RT_FAULT_REJECT) m += " a rejection sampler exceeded its attempt cap;";
-    if (f & RT_FAULT_CURVE) m += " a curve walk exceeded its step bound;";
+    if (f & RT_FAULT_CURVE) m += " a curve walk exceeded its step bound or a curve needed more subdivision levels than the walk supports;";
     if (f & RT_FAULT_PATH) m += " a persistent kernel's path or ray exceeded its step bound;";
     if (f & RT_FAULT_SHARD) m += " a queue shard overflowed (the append was dropped);";
     if (f & RT_FAULT_LDS) m += " a persistent kernel's LDS allocation was too small;";
@@ -1076,11 +1076,6 @@ size_t max_paths(const int lanes) {
 int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = no overlap)
     const char* e = std::getenv("RTAMD_LANES");
     return e ? std::max(1, std::atoi(e)) : 2;
-}
-
-bool debug_counts() {
-    static const bool v = std::getenv("RTAMD_DEBUG_COUNTS") != nullptr;
-    return v;
 }
 
 uint32_t tail_threshold() {
@@ -1130,6 +1125,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     {
         uint32_t stale = 0;
         HIPCHK(take_fault(&stale));                  // a fault word left by another context's failed launch
+        unsigned long long cs[2];
+        HIPCHK(take_curve_stats(cs));                // counters start at zero for this render
         const char* e = std::getenv("RTAMD_REJECT_CAP");  // tests: drive a sampler into its cap
         HIPCHK(set_reject_cap(e ? std::max(0, std::atoi(e)) : 4096));
     }
@@ -1153,16 +1150,13 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // for a third of it).  A floor of four cost 6.5 % on a 1/8-frame shard
     // (680x381x1024 spp, the per-rank work at 8 GPUs) and 2.4 % at 1/4
     // (profiles/r02/mc/).
-    // the cap is sized on the scene's first render (before its own pools exist), then kept
-    if (!s->pool_cap || std::getenv("RTAMD_MAX_PATHS")) s->pool_cap = max_paths(std::min(kLanes, lanes_wanted()));
-    const size_t cap_paths = s->pool_cap;
+    // the cap is sized on the context's first render (before its pools exist), then kept
+    if (!c->pool_cap || std::getenv("RTAMD_MAX_PATHS")) c->pool_cap = max_paths(std::min(kLanes, lanes_wanted()));
+    const size_t cap_paths = c->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     {
-        static const int min_chunks = [] {          // RTAMD_MIN_CHUNKS (A/B; default 2)
-            const char* e = std::getenv("RTAMD_MIN_CHUNKS");
-            return e ? std::max(1, std::atoi(e)) : 2;
-        }();
+        constexpr int min_chunks = 2;
         int n = (int)((spp_count + chunk - 1) / chunk);
         if (n < min_chunks) n = std::min(min_chunks, spp_count);
         if (n > 1 && (n & 1) && n < spp_count) ++n;
@@ -1188,8 +1182,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     std::unique_ptr<void, void (*)(void*)> ev_in_guard(ev_in, [](void* e) { (void)hipEventDestroy((hipEvent_t)e); });
     HIPCHK(hipEventRecord(ev_in, stream));
     for (int li = 0; li < nlanes; ++li) {
-        if (!s->lanes[li]) s->lanes[li].reset(new Lane());
-        Lane& L = *s->lanes[li];
+        if (!c->lanes[li]) c->lanes[li].reset(new Lane());
+        Lane& L = *c->lanes[li];
         if (!L.stream) HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
         if (!L.ev_cnt) HIPCHK(hipEventCreateWithFlags(&L.ev_cnt, hipEventDisableTiming));
         if (!L.ev_acc) HIPCHK(hipEventCreateWithFlags(&L.ev_acc, hipEventDisableTiming));
@@ -1211,15 +1205,15 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // An error return below leaves kernels queued on the lanes that may still
     // write the caller's accumulator: drain every lane before returning.
     struct Drain {
-        Scene* s; int n; bool armed = true;
+        Context* c; int n; bool armed = true;
         ~Drain() {
             if (!armed) return;
             for (int i = 0; i < n; ++i)
-                if (s->lanes[i] && s->lanes[i]->stream) (void)hipStreamSynchronize(s->lanes[i]->stream);
+                if (c->lanes[i] && c->lanes[i]->stream) (void)hipStreamSynchronize(c->lanes[i]->stream);
             uint32_t f = 0;
             (void)take_fault(&f);                  // do not leak this render's fault bits into the next
         }
-    } drain{s, nlanes};
+    } drain{c, nlanes};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     uint64_t seq = 0;
 
@@ -1307,7 +1301,6 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         std::swap(L.cur, L.nxt);
         L.n = n;
         ++L.depth;
-        if (debug_counts() && L.chunk == 0) std::fprintf(stderr, "rtamd: chunk 0 depth %d paths %u\n", L.depth, n);
         return step(L);
     };
     auto start = [&](Lane& L, int ch) -> int {
@@ -1333,7 +1326,6 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         L.n = rp.B;
         L.depth = 0;
         s->stats.paths += rp.B;
-        if (debug_counts() && ch == 0) std::fprintf(stderr, "rtamd: chunk 0 depth 0 paths %u\n", L.n);
         return step(L);
     };
 
@@ -1342,7 +1334,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     while (next_acc < nchunks) {
         bool progressed = false;
         for (int li = 0; li < nlanes; ++li) {           // accumulate in chunk order
-            Lane& L = *s->lanes[li];
+            Lane& L = *c->lanes[li];
             if (L.state != Lane::DONE || L.chunk != next_acc) continue;
             if (last_acc && last_acc != &L) HIPCHK(hipStreamWaitEvent(L.stream, last_acc->ev_acc, 0));
             HIPCHK(launch_accumulate(L.rp, L.S, accum, L.stream));
@@ -1354,13 +1346,13 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             li = -1;                                     // the next chunk may sit on an earlier lane
         }
         for (int li = 0; li < nlanes; ++li) {           // idle lanes take the next chunk
-            Lane& L = *s->lanes[li];
+            Lane& L = *c->lanes[li];
             if (L.state != Lane::IDLE || next_chunk >= nchunks) continue;
             if (int rc = start(L, next_chunk++)) return rc;
             progressed = true;
         }
         for (int li = 0; li < nlanes; ++li) {           // lanes whose counts have arrived
-            Lane& L = *s->lanes[li];
+            Lane& L = *c->lanes[li];
             if (L.state != Lane::RUNNING) continue;
             const hipError_t q = hipEventQuery(L.ev_cnt);
             if (q == hipErrorNotReady) continue;
@@ -1371,21 +1363,25 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         if (progressed) continue;
         Lane* oldest = nullptr;                          // nothing to do: wait for the oldest pending step
         for (int li = 0; li < nlanes; ++li) {
-            Lane& L = *s->lanes[li];
+            Lane& L = *c->lanes[li];
             if (L.state == Lane::RUNNING && (!oldest || L.seq < oldest->seq)) oldest = &L;
         }
         if (!oldest) return fail("internal: render lanes stalled");
         HIPCHK(hipEventSynchronize(oldest->ev_cnt));
     }
-    for (int li = 0; li < nlanes; ++li) HIPCHK(hipStreamSynchronize(s->lanes[li]->stream));
+    for (int li = 0; li < nlanes; ++li) HIPCHK(hipStreamSynchronize(c->lanes[li]->stream));
     drain.armed = false;
     {
         uint32_t f = 0;
         HIPCHK(take_fault(&f));
         if (f) return fail(fault_text(f));
+        unsigned long long cs[2];
+        HIPCHK(take_curve_stats(cs));
+        s->stats.curve_pooled_batches = cs[0];
+        s->stats.curve_flat_pooled = cs[1];
     }
     for (int li = 0; li < nlanes; ++li) {
-        Lane& L = *s->lanes[li];
+        Lane& L = *c->lanes[li];
         unsigned long long ctl[3] = {0, 0, 0};
         HIPCHK(hipMemcpy(ctl, L.seg_tail.p, sizeof ctl, hipMemcpyDeviceToHost));
         if (ctl[2]) return fail("internal: a persistent kernel's LDS allocation was too small (flags " +
@@ -1445,6 +1441,18 @@ int rt_context_destroy(int ctx) {
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     g_ctx.erase(ctx);
+    return 0;
+}
+
+int rt_context_release_pools(int ctx) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    HIPCHK(hipSetDevice(c->device));
+    for (auto& L : c->lanes)
+        if (L && L->stream) HIPCHK(hipStreamSynchronize(L->stream));
+    for (auto& L : c->lanes) L.reset();
+    c->pool_cap = 0;                               // the next render sizes them again
     return 0;
 }
 
@@ -1771,6 +1779,36 @@ int rt_get_scene_info(int scene, rt_scene_info* out) {
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     out->cus = cus;
+    return 0;
+}
+
+int rt_hit_rays(int scene, int n, const double* rays, double* out_t, int32_t* out_mat) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scene* s = get_scene(scene);
+    if (!s) return fail("invalid scene handle");
+    if (!s->committed) return fail("scene not committed (rt_scene_commit)");
+    if (n < 0) return fail("ray count must be >= 0");
+    if (n > 0 && (!rays || !out_t || !out_mat)) return fail("null pointer");
+    if (s->dev.n_med > 0) return fail("rt_hit_rays: the scene has constant media, whose hit test draws random numbers");
+    Context* c = get_ctx(s->ctx);
+    if (!c) return fail("scene's context was destroyed");
+    if (n == 0) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t stale = 0;
+    HIPCHK(take_fault(&stale));
+    DevBuf d_rays, d_t, d_mat;
+    HIPCHK(d_rays.ensure((size_t)n * 7 * sizeof(double)));
+    HIPCHK(d_t.ensure((size_t)n * sizeof(double)));
+    HIPCHK(d_mat.ensure((size_t)n * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(d_rays.p, rays, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_hit_rays(s->dev, d_rays.as<const double>(), (uint32_t)n, d_t.as<double>(), d_mat.as<int32_t>(),
+                           c->stream));
+    HIPCHK(hipMemcpyAsync(out_t, d_t.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out_mat, d_mat.p, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint32_t f = 0;
+    HIPCHK(take_fault(&f));
+    if (f) return fail(fault_text(f));
     return 0;
 }
 

@@ -52,11 +52,11 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;      // block_append / wave_append: th
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
                                          uint32_t k0, uint32_t k1) {
-#ifndef RT_PHILOX_ROUNDS
-#define RT_PHILOX_ROUNDS 10     // A/B builds only; 10 is the stream's definition
-#endif
+    // Philox4x32-10: ten rounds define the stream the oracle restates
+    // (oracle/rt_oracle.c philox4x32_10); no build may change them
+    constexpr int kPhiloxRounds = 10;
 #pragma unroll
-    for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
+    for (int r = 0; r < kPhiloxRounds; ++r) {
         if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         // one 32x32->64 product per word (v_mad_u64_u32) instead of separate
         // low / high multiplies: 1.36x the Philox rate (tools micro-benchmark)
@@ -330,8 +330,10 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
         l0 = fmax(fmax(x1, y1), l0);
     }
     const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / B.eps8) / log(4.0);
-    int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
-    if (maxd > kBezMaxDepth) maxd = kBezMaxDepth;   // beyond any width / extent ratio a scene uses
+    const int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
+    // converge has no depth limit (bezier.scm:189-193); a curve needing more
+    // levels than the walk's 32-bit node index holds fails the render loudly
+    if (!(maxd <= kBezMaxDepth)) { raise_fault(RT_FAULT_CURVE); return false; }
     bool found = false;
     double best = tmax;
     // Depth-first walk of the subdivision tree without a stack: node (L, idx)
@@ -418,8 +420,8 @@ __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
     const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
     l0 = fmax(fmax(x1, y1), l0);
     const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / eps8) / log(4.0);
-    const int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
-    return maxd > kBezMaxDepth ? kBezMaxDepth : maxd;
+    // saturates at kBezMaxDepth + 1: the caller faults on anything deeper than the walk supports
+    return (md == -INFINITY) ? 0 : (md > (double)(kBezMaxDepth + 1) ? kBezMaxDepth + 1 : (int)ceil(md));
 }
 // set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
 // stage A's root cull) is given; false if the whole curve is culled
@@ -506,12 +508,7 @@ __device__ unsigned long long g_stats[32];
 // curve's answer does not depend on the t-max it is tested with, beyond
 // being reported only when z <= t-max (see bezier_test), so deferring the
 // tests changes no result.
-#ifndef RT_BEZ_FLAT
-#define RT_BEZ_FLAT 1                  // stage B as a refilling per-lane walk (0: one curve per lane per pass)
-#endif
-#ifndef RT_BEZ_REFILL
-#define RT_BEZ_REFILL 8                // idle lanes that take the next survivors together
-#endif
+constexpr int kBezRefill = 8;         // stage B: idle lanes that take the next survivors together
 constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
 #ifndef RT_BEZ_HOLD
 #define RT_BEZ_HOLD 192                // stage B runs once this many root-cull survivors wait (multiple of 64)
@@ -554,8 +551,13 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
             Bez4 c;
             bez_load(B, W.ray[e & 63u], c);
             keep = !bez_culled(c, B.w1, W.cl[e & 63u]);
-            // leaf level maxd + 1, at least 0: a flat curve's maxd is negative (its root is a leaf)
-            if (keep) lev = (uint8_t)max(0, bez_maxd(c, B.eps8) + 1);
+            // leaf level maxd + 1, at least 0: a flat curve's maxd is negative (its root is a leaf);
+            // converge has no depth limit (bezier.scm:189-193): deeper than the walk supports fails loudly
+            if (keep) {
+                const int maxd = bez_maxd(c, B.eps8);
+                if (maxd > kBezMaxDepth) { raise_fault(RT_FAULT_CURVE); keep = false; }
+                else lev = (uint8_t)max(0, maxd + 1);
+            }
             if (TRACK && !keep) atomicAdd(&W.done[e & 63u], 1u);
         }
         const unsigned long long m = __ballot(keep);
@@ -572,13 +574,27 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
 // Stage B: full subdivision of the first nb survivors, one per lane, then per
 // owner the smallest z (ties: smallest curve index) into hz / hid; the
 // remaining svn - nb survivors move to the front.
+// Pooled-curve counters (rt_stats.curve_pooled_batches / curve_flat_pooled):
+// stage B passes over a full pool (>= RT_BEZ_HOLD survivors), and the
+// survivors they walked whose root is already a leaf (a flat curve: converge's
+// depth estimate is negative, bezier.scm:130,189-193).  One atomic per pass;
+// read and cleared by take_curve_stats.
+__device__ unsigned long long g_curve_stats[2];
 template <bool TRACK = false>
 __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
-#if RT_BEZ_FLAT
+    if (nb >= (uint32_t)RT_BEZ_HOLD) {
+        uint32_t flat = 0;
+        for (uint32_t base = 0; base < nb; base += nact)
+            flat += (uint32_t)__popcll(__ballot(base + rank < nb && W.lev[base + rank] == 0));
+        if (rank == 0) {
+            atomicAdd(&g_curve_stats[0], 1ull);
+            if (flat) atomicAdd(&g_curve_stats[1], (unsigned long long)flat);
+        }
+    }
     // Lanes take survivors one after the other from a wave-uniform cursor and
-    // walk them a node per iteration (BezWalk): when at least RT_BEZ_REFILL
+    // walk them a node per iteration (BezWalk): when at least kBezRefill
     // lanes are idle they take the next survivors together, so a lane is not
     // held by the longest walk of a fixed batch of 64.
     {
@@ -589,7 +605,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         for (unsigned long long g = 0;; ++g) {                    // wave-uniform
             if (g > guard_cap) { raise_fault(RT_FAULT_CURVE); break; }
             const unsigned long long idle = __ballot(!busy);
-            if (cursor < nb && (__popcll(idle) >= RT_BEZ_REFILL || idle == act)) {
+            if (cursor < nb && (__popcll(idle) >= kBezRefill || idle == act)) {
                 if (!busy) {
                     const uint32_t i = cursor + lanes_below(idle);
                     if (i < nb) {
@@ -611,16 +627,6 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             }
         }
     }
-#else
-    for (uint32_t base = 0; base < nb; base += nact) {
-        const uint32_t i = base + rank;
-        if (i < nb) {
-            const uint32_t e = W.sv[i];
-            double t;
-            W.sz[i] = bezier_test(sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], t) ? t : INFINITY;
-        }
-    }
-#endif
     wave_sync();
     for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
@@ -694,9 +700,6 @@ __device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, con
 // near / far plane pairs (left, right) in a BvhNode2.
 #ifndef RT_SIGNED_SLAB
 #define RT_SIGNED_SLAB 1
-#endif
-#ifndef RT_SEARCH_MAX
-#define RT_SEARCH_MAX 0                // the walk's leaf phase starts once at most this many lanes lack a parked leaf
 #endif
 struct SlabOff { uint32_t nx, ny, nz, fx, fy, fz; };
 __device__ __forceinline__ SlabOff slab_off(const BoxRay& r) {
@@ -807,8 +810,8 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                     node = sp ? stack_ref(lstk[sp -= stride]) : kDone;
                 }
             }
-            // every active lane has a leaf parked (RT_SEARCH_MAX: or at most that many still search)
-            if ((uint32_t)__popcll(__ballot(pend == kDone)) <= (uint32_t)RT_SEARCH_MAX) break;
+            // every active lane has a leaf parked
+            if (__ballot(pend == kDone) == 0ull) break;
         }
         if (pend != kDone) {
             if constexpr (DIRECT) {
@@ -1310,7 +1313,9 @@ __device__ __forceinline__ QMap qmap(const QView v) {
     m.contiguous = v.counts == nullptr;
     uint32_t acc = 0;
 #pragma unroll
-    for (int x = 0; x < kShards; ++x) { m.off[x] = acc; if (!m.contiguous) acc += v.counts[x * kCntStride]; }
+    // a shard's counter can pass its capacity (the append then dropped the item and
+    // raised RT_FAULT_SHARD): consumers index only what was written
+    for (int x = 0; x < kShards; ++x) { m.off[x] = acc; if (!m.contiguous) acc += min(v.counts[x * kCntStride], v.cap); }
     return m;
 }
 __device__ __forceinline__ uint32_t qphys(const QMap& m, uint32_t k) {
@@ -1413,6 +1418,31 @@ __global__ __launch_bounds__(256) void k_extend(const DevScene sc, const RenderP
     if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
 }
 
+// =====================================================================
+// k_hit_rays — the world's closest hit for a caller's batch of rays
+// (rt_hit_rays; hit-obj-list geometry.scm:33-50 over the scene list, as the
+// integrator calls it at main.scm:104): t and the leaf's material, or -1.
+// The same closest_hit<F> the extend kernels run; a diagnostic / test probe,
+// not on the render path.  Scenes with media are refused by the host (the
+// medium's hit test draws from the path's random stream).
+// =====================================================================
+template <int F>
+__global__ __launch_bounds__(256) void k_hit_rays(const DevScene sc, const double* __restrict__ rays, uint32_t n,
+                                                  double* __restrict__ out_t, int32_t* __restrict__ out_mat) {
+    extern __shared__ uint32_t s_lstack[];
+    constexpr bool BEZ = (F & kFeatCurves) != 0;
+    __shared__ BezWave s_bw[BEZ ? 4 : 1];
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= n) return;
+    const double* r = rays + 7 * (size_t)k;
+    double t = 0.0;
+    const int32_t leaf = closest_hit<F>(sc, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6], t,
+                                        s_lstack + threadIdx.x, sc.lane_stack, &s_bw[BEZ ? (threadIdx.x >> 6) : 0],
+                                        nullptr, tree0_hbm(sc), treeA_hbm(sc));
+    out_t[k] = leaf < 0 ? 0.0 : t;
+    out_mat[k] = leaf < 0 ? -1 : sc.leaves[leaf].mat;
+}
+
 // Wave-level append into the sharded material queues (block_append's layout:
 // class c, shard x -> counter (c * kShards + x), slot x * shard_cap + rank)
 // for kernels whose lanes finish at different loop iterations.  One atomic
@@ -1477,15 +1507,19 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
     BvhNode2 N{};                                   // the lane's next node, loaded one iteration ahead
     int sp = 0, pb = 0, pe = 0;
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
-    // a ray takes at most one step per node / leaf and one queue step per two curves, and waits for
-    // batches that other lanes' steps trigger: bound its loop iterations (a valid walk stays far below)
+    // a ray takes at most one step per node / leaf and one queue step per two curves: bound its
+    // working iterations (a valid walk stays far below)
     const uint32_t ray_cap = 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
     uint32_t ray_it = 0;
 #ifdef RT_STATS
     uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
 #endif
     for (;;) {
-        if (active && ++ray_it > ray_cap) { raise_fault(RT_FAULT_PATH); active = false; trav = false; pb = pe; }
+        // only iterations in which the lane itself works count: one waiting for a batch
+        // other lanes trigger is bounded by their work (the last batch runs once no lane can add)
+        if (active && (trav || pb < pe) && ++ray_it > ray_cap) {
+            raise_fault(RT_FAULT_PATH); active = false; trav = false; pb = pe;
+        }
 #ifdef RT_STATS
         ++st_iter;
         if (active && trav && pb >= pe) ++st_steps;
@@ -1658,25 +1692,18 @@ __device__ __forceinline__ void stage_lds(T* dst, const T* src, const int n, con
     for (int k = threadIdx.x; k < words; k += nthreads) l[k] = g[k];
 }
 
-// Work distribution and hit-queue append of the persistent LDS kernels.
-// Block mode: a block takes kExtLdsBlock consecutive items per grid-stride
-// step and appends them with block_append (one atomic per block and class,
-// three barriers).  Wave mode (RT_EXT_WAVE_APPEND): each wave takes its own 64
-// of those items and appends with wave_append (one atomic per wave and
-// class, no barrier), so a wave is never held by a slower wave of its block.
-// Same items, same shard (blockIdx % kShards); queue order differs, images do
-// not (a path's result does not depend on its queue position).
-#ifndef RT_EXT_WAVE_APPEND
-#define RT_EXT_WAVE_APPEND 1
-#endif
-__device__ __forceinline__ uint32_t ext_first() {
-    return blockIdx.x * kExtLdsBlock + (RT_EXT_WAVE_APPEND ? (threadIdx.x & ~63u) : 0u);
-}
-__device__ __forceinline__ uint32_t ext_lid() { return RT_EXT_WAVE_APPEND ? (threadIdx.x & 63u) : threadIdx.x; }
+// Work distribution and hit-queue append of the persistent LDS kernels: a
+// block takes kExtLdsBlock consecutive items per grid-stride step, each wave
+// its own 64 of them, appended with wave_append (one atomic per wave and
+// class, no barrier), so a wave is never held by a slower wave of its block
+// (against block_append's one atomic per block and three barriers: +3 %).
+// Items keep their shard (blockIdx % kShards); queue order does not change
+// images (a path's result does not depend on its queue position).
+__device__ __forceinline__ uint32_t ext_first() { return blockIdx.x * kExtLdsBlock + (threadIdx.x & ~63u); }
+__device__ __forceinline__ uint32_t ext_lid() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t ext_append(const int cls, uint32_t* __restrict__ counts, const uint32_t shard_cap,
-                                               uint32_t* s_cnt) {
-    if (RT_EXT_WAVE_APPEND) return wave_append(cls, blockIdx.x & (uint32_t)(kShards - 1), counts, shard_cap);
-    return block_append<4>(cls, counts, shard_cap, s_cnt);
+                                               uint32_t*) {
+    return wave_append(cls, blockIdx.x & (uint32_t)(kShards - 1), counts, shard_cap);
 }
 
 // Dynamic LDS the persistent kernels carve (host and device use the same
@@ -2193,13 +2220,6 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 #endif
 template <int MAT>
 constexpr int shade_waves() { return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD : RT_SHADE_WAVES; }
-#ifndef RT_SHADE_PREFETCH
-#define RT_SHADE_PREFETCH 0
-#endif
-template <int MAT>
-constexpr bool shade_prefetch() {
-    return RT_SHADE_PREFETCH == 2 || (RT_SHADE_PREFETCH == 1 && (MAT == MAT_METAL || MAT == MAT_DIELECTRIC));
-}
 template <int MAT, bool PN, bool LS, bool LL>
 __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
                                                                 const PathState in, const HitRec* __restrict__ hq,
@@ -2220,23 +2240,15 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
     const QMap qm = qmap(qv);
     uint32_t n = 0;
 #pragma unroll
-    for (int x = 0; x < kShards; ++x) n += qv.counts[x * kCntStride];
-    // PF: the next grid-stride item's queue entry is loaded while this item is
-    // shaded, so an iteration starts with its ray / path gather instead of a
-    // dependent queue load first (RT_SHADE_PREFETCH: 1 = metal / dielectric,
-    // 2 = every material)
-    constexpr bool PF = shade_prefetch<MAT>();
+    for (int x = 0; x < kShards; ++x) n += min(qv.counts[x * kCntStride], qv.cap);   // written entries only
     const uint32_t gstride = gridDim.x * 256u;
-    HitRec Hn{};
-    if (PF && blockIdx.x * 256u + threadIdx.x < n) Hn = hq[qphys(qm, blockIdx.x * 256u + threadIdx.x)];
     for (uint32_t base = blockIdx.x * 256u; base < n; base += gstride) {
         const uint32_t k = base + threadIdx.x;
         bool alive = false;
         PathRegs p;
         if (k < n) {
-            const HitRec H = PF ? Hn : hq[qphys(qm, k)];
+            const HitRec H = hq[qphys(qm, k)];
             load_path(in, H.slot, p, rp, depth);
-            if (PF && k + gstride < n) Hn = hq[qphys(qm, k + gstride)];
             v3 L;
             alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
             if (!alive) write_sample(rp, p, L);
@@ -2382,14 +2394,7 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     hipLaunchKernelGGL(k_raygen, dim3(blocks), dim3(256), 0, s, sc, rp, st);
     return hipGetLastError();
 }
-static uint32_t finish_blocks() {            // persistent tail grid (RTAMD_FINISH_BLOCKS)
-    static const uint32_t v = [] {
-        const char* e = std::getenv("RTAMD_FINISH_BLOCKS");
-        const long b = e ? std::atol(e) : 512;
-        return (uint32_t)(b > 0 ? b : 512);
-    }();
-    return v;
-}
+static uint32_t finish_blocks() { return 512u; }   // persistent tail grid
 static bool finish_generic() {               // RTAMD_FINISH_GENERIC: the group-loop tail for SOLO scenes too (A/B, tests)
     const char* e = std::getenv("RTAMD_FINISH_GENERIC");  // read per launch: tests switch it inside one process
     return e != nullptr && e[0] != '0';
@@ -2435,6 +2440,20 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
     default: RT_EXTEND_F(3); break;
     }
 #undef RT_EXTEND_F
+    return hipGetLastError();
+}
+hipError_t launch_hit_rays(const DevScene& sc, const double* rays, uint32_t n, double* out_t, int32_t* out_mat,
+                           hipStream_t s) {
+    const uint32_t blocks = (n + 255u) / 256u;
+    const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
+    if (!blocks) return hipSuccess;
+    switch (scene_features(sc)) {
+    case 0: hipLaunchKernelGGL((k_hit_rays<0>), dim3(blocks), dim3(256), lds, s, sc, rays, n, out_t, out_mat); break;
+    default:
+        hipLaunchKernelGGL((k_hit_rays<kFeatCurves | kFeatExtra>), dim3(blocks), dim3(256), lds, s, sc, rays, n, out_t,
+                           out_mat);
+        break;
+    }
     return hipGetLastError();
 }
 // bytes of LDS k_extend_lds needs for the scene's time-0 tree (0 = cannot run)
@@ -2510,21 +2529,13 @@ hipError_t launch_camera(const DevScene& sc, const RenderParams& rp, const PathS
     return hipGetLastError();
 }
 constexpr size_t kShadeLeafLds = 32768;      // stage the leaf records when they fit (256 leaves)
-static bool shade_leaves_hbm() {             // RTAMD_SHADE_LEAVES_HBM: keep them in HBM (A/B)
-    static const bool v = std::getenv("RTAMD_SHADE_LEAVES_HBM") != nullptr;
-    return v;
-}
 hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& in,
                         const HitBuf& hit, const QView& qv, uint32_t n_upper,
                         const PathState& out, uint32_t* out_counts, uint32_t shard_cap, uint32_t depth, hipStream_t s) {
     // grid-stride cap: each block stages the leaf records once, so fewer,
     // longer-lived blocks (2048 was best of 1024..8192 with 96M-path pools;
     // 1024 with the 288M-path pools: +1.5 % C2, 512 -14 %: profiles/r02/shadeb/)
-    static const uint32_t max_blocks = [] {          // RTAMD_SHADE_BLOCKS (A/B)
-        const char* e = std::getenv("RTAMD_SHADE_BLOCKS");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1024ul;
-        return (uint32_t)(v >= 4096 ? 4096 : v >= 8 ? v / 8 * 8 : 8);   // rt_api's shard slack assumes <= 4096
-    }();
+    constexpr uint32_t max_blocks = 1024;            // (rt_api's shard slack assumes <= 4096, a multiple of 8)
     uint32_t blocks = (n_upper + 255u) / 256u;
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > max_blocks) blocks = max_blocks;
@@ -2542,7 +2553,7 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
     const size_t leaf_lds = (size_t)sc.n_leaves * sizeof(LeafInfo);
-    const bool ll = leaf_lds <= kShadeLeafLds && !shade_leaves_hbm();
+    const bool ll = leaf_lds <= kShadeLeafLds;
     // PN kernels of every material carry the Perlin tables (metal albedo may be a noise texture)
     const size_t lds = (ll ? leaf_lds : 0) + ((pn && mat != MAT_DIELECTRIC && sc.has_perlin) ? sizeof(PerlinLds) : 0);
     switch (mat) {
@@ -2623,6 +2634,15 @@ hipError_t take_fault(uint32_t* out) {
         HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_fault), &z, sizeof z));
     }
     *out = f;
+    return hipSuccess;
+}
+// the batched-curve counters: read and clear (render_impl, at the start and end of a render)
+hipError_t take_curve_stats(unsigned long long out[2]) {
+    HIP_RETURN_IF(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_curve_stats), 2 * sizeof(unsigned long long)));
+    if (out[0] || out[1]) {
+        const unsigned long long z[2] = {0ull, 0ull};
+        HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_curve_stats), z, sizeof z));
+    }
     return hipSuccess;
 }
 #ifdef RT_STATS

@@ -40,6 +40,8 @@ class RtStats(ctypes.Structure):
         ("shade_survivors", ctypes.c_uint64),
         ("chunks", ctypes.c_uint32),
         ("lanes", ctypes.c_uint32),
+        ("curve_pooled_batches", ctypes.c_uint64),
+        ("curve_flat_pooled", ctypes.c_uint64),
     ]
 
 
@@ -57,6 +59,9 @@ _SIGNATURES = {
     "rt_device_count": [_c_int_p],
     "rt_context_create": [ctypes.c_int, _c_int_p],
     "rt_context_destroy": [ctypes.c_int],
+    "rt_context_release_pools": [ctypes.c_int],
+    "rt_hit_rays": [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                    ctypes.POINTER(ctypes.c_int32)],
     "rt_scene_begin": [ctypes.c_int, _c_int_p],
     "rt_scene_destroy": [ctypes.c_int],
     "rt_add_texture_constant": [ctypes.c_int, _c_double_p, _c_int_p],

@@ -20,6 +20,7 @@ import numpy as np
 from . import gpu
 
 _pix_cache = {}
+_dev_cache = {}
 
 
 def shard_pixels(nx, ny, world):
@@ -30,10 +31,29 @@ def shard_pixels(nx, ny, world):
     return _pix_cache[key]
 
 
-def gather_frame(local, nx, ny, rank, world, group=None):
+def _gather_buffers(nx, ny, world, dtype, dev, frame_dev):
+    """The exchange's buffers, made once per (frame, world, device) and kept:
+    the padded send buffer, rank 0's receive buffers, and every rank's pixel
+    index list already on rank 0's device (no host upload per frame)."""
+    import torch
+    key = (nx, ny, world, dtype, str(dev), str(frame_dev))
+    if key not in _dev_cache:
+        pix = shard_pixels(nx, ny, world)
+        width = 3 * max(len(p) for p in pix)    # collectives move equal-size buffers: pad to the largest shard
+        _dev_cache[key] = {
+            "send": torch.zeros(width, dtype=dtype, device=dev),
+            "recv": None,                       # rank 0 only (gather_frame)
+            "idx": [torch.from_numpy(p).to(frame_dev) for p in pix],
+        }
+    return _dev_cache[key]
+
+
+def gather_frame(local, nx, ny, rank, world, group=None, out=None):
     """Gather every rank's compact accumulator (a 1-D float64 tensor of
-    3 x its pixel count) onto rank 0 and scatter it into an nx*ny*3 frame.
-    Returns the frame on rank 0 (on local's device), None on other ranks."""
+    3 x its pixel count) onto rank 0 and scatter it into an nx*ny*3 frame
+    (``out`` if given, else a new tensor on local's device).  Returns the
+    frame on rank 0, None on other ranks.  Shards differ by at most one
+    16x16 tile, so padding them to equal size moves < 6 KB more per rank."""
     import torch
     import torch.distributed as dist
 
@@ -41,24 +61,25 @@ def gather_frame(local, nx, ny, rank, world, group=None):
     counts = [len(p) for p in pix]
     if local.numel() != 3 * counts[rank]:
         raise ValueError("rank %d holds %d values, its shard has %d pixels" % (rank, local.numel(), counts[rank]))
-    width = 3 * max(counts)                     # collectives move equal-size buffers: pad to the largest shard
     # RCCL gathers device buffers; gloo (CPU tests, one-GPU rehearsals of the
     # multi-process bench) gathers host copies
     dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else local.device
-    send = local.to(dev)
-    if local.numel() < width:
-        send = torch.zeros(width, dtype=local.dtype, device=dev)
-        send[:local.numel()] = local.to(dev)
-    bufs = [torch.empty(width, dtype=local.dtype, device=dev) for _ in range(world)] if rank == 0 else None
-    dist.gather(send, gather_list=bufs, dst=0, group=group)
+    B = _gather_buffers(nx, ny, world, local.dtype, dev, local.device)
+    send = B["send"]
+    send[:local.numel()].copy_(local)
+    if rank == 0 and B["recv"] is None:
+        B["recv"] = [torch.empty_like(send) for _ in range(world)]
+    dist.gather(send, gather_list=B["recv"] if rank == 0 else None, dst=0, group=group)
     if rank != 0:
         return None
-    frame = torch.zeros(nx * ny * 3, dtype=local.dtype, device=local.device)
-    rows = frame.view(-1, 3)
+    if out is None:
+        out = torch.empty(nx * ny * 3, dtype=local.dtype, device=local.device)
+    if out.numel() != nx * ny * 3:
+        raise ValueError("out must hold nx*ny*3 values")
+    rows = out.view(-1, 3)                      # the shards cover every pixel exactly once
     for r in range(world):
-        idx = torch.from_numpy(pix[r]).to(local.device)
-        rows.index_copy_(0, idx, bufs[r][:3 * counts[r]].view(-1, 3).to(local.device))
-    return frame
+        rows.index_copy_(0, B["idx"][r], B["recv"][r][:3 * counts[r]].view(-1, 3).to(local.device))
+    return out
 
 
 def render_frame(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local=None, frame=None, stream=None,
@@ -66,7 +87,7 @@ def render_frame(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local=N
     """One frame's passes on this rank's GPU.  world == 1: straight into `frame`
     (a full-frame device tensor).  world > 1: this rank's tiles into `local`
     (compact, 3 x shard pixels, zeroed by the caller), then gather_frame;
-    returns the frame on rank 0 and None elsewhere."""
+    returns the frame (``frame`` if given) on rank 0 and None elsewhere."""
     if stream is None:                          # order after the caller's torch work (e.g. zeroing the buffers)
         import torch
         stream = torch.cuda.current_stream().cuda_stream
@@ -75,7 +96,7 @@ def render_frame(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local=N
         return frame
     gpu.render_shard_device(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local.data_ptr(), stream=stream,
                             ctx=ctx)
-    return gather_frame(local, nx, ny, rank, world)
+    return gather_frame(local, nx, ny, rank, world, out=frame)
 
 
 def local_size(nx, ny, rank, world):

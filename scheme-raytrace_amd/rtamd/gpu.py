@@ -20,6 +20,11 @@ class Context:
         self.handle = h.value
         self.device = device
 
+    def release_pools(self):
+        """rt_context_release_pools: free the render lanes' path pools (the
+        next render on this context allocates and sizes them again)."""
+        call("rt_context_release_pools", self.handle)
+
     def close(self):
         if self.handle:
             call("rt_context_destroy", self.handle)
@@ -226,6 +231,19 @@ def render_shard_device(scene, nx, ny, spp_begin, spp_count, seed, shard, nshard
     call("rt_render_shard_device", h, nx, ny, spp_begin, spp_count, ctypes.c_uint64(seed & (2**64 - 1)), shard,
          nshard, ctypes.c_void_p(accum_ptr), ctypes.c_void_p(stream or 0))
     return h
+
+
+def hit_rays(scene, rays, ctx=None):
+    """rt_hit_rays: rays = (n, 7) float64 (origin, direction, time); returns
+    (t, material id) arrays, material -1 for a miss."""
+    h = upload(scene, ctx)
+    r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 7)
+    n = r.shape[0]
+    t = np.zeros(n)
+    m = np.zeros(n, dtype=np.int32)
+    call("rt_hit_rays", h, n, r.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+         t.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), m.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return t, m
 
 
 def resolve_u8(accum, nx, ny, sample_count):

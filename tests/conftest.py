@@ -9,6 +9,20 @@ for p in (os.path.join(ROOT, "scheme-raytrace_amd"), os.path.join(ROOT, "oracle"
         sys.path.insert(0, p)
 
 
+def host_threads():
+    """Threads for the oracle on this host: the process's CPU share (a GPU box
+    gives a one-GPU job 16 CPUs of a much larger machine; os.cpu_count()
+    reports the machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, 64))
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests proper")
     config.addinivalue_line("markers", "slow: long-running CPU test")

@@ -1,0 +1,146 @@
+"""GPU tests of the curve path (bezier.scm:13-223) at configuration C5's scale.
+
+* C5 itself — 2^20 curves in a BVH (geometry.scm:294-371 as test-bezier and
+  cornell-bezier use it) at 1920x1080 — on a band of rows through the curve
+  cloud, at the top sample indices of the 256-spp frame, on the production
+  schedule (several chunks on two render lanes: k_camera / k_extend_curves /
+  k_shade for the wide iterations, k_finish for the tail), against the oracle
+  (whose OBJ_BVH is a tree with the flat list's semantics,
+  tests/test_oracle_bvh.py).
+* Flat curves — converge's depth estimate negative, so the root is a leaf
+  (bezier.scm:130,189-193) — pooled into the wavefront curve kernel's batched
+  subdivision (stage B over >= RT_BEZ_HOLD survivors), counted by
+  rt_stats.curve_flat_pooled: the case whose negative leaf level faulted C5 in
+  round 2 before the level was clamped at 0.
+* A curve needing more subdivision levels than the walk supports fails the
+  render with the curve fault (the reference has no depth limit).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import host_threads
+from rtamd import gpu, scenes
+from rtamd import scene as g
+from rtamd import vec as v
+from rtamd._lib import RtError
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4
+SEED = 0x5EED0002
+
+
+def _compare(a, b, n):
+    d = np.abs(a / n - b / n)
+    px = d.reshape(-1, 3).max(axis=1)
+    return float(np.sqrt(np.mean(d ** 2))), float(d.max()), int((px > 1e-9).sum()), px.size
+
+
+def _env(monkeypatch, **kv):
+    for k, val in kv.items():
+        monkeypatch.setenv(k, str(val))
+
+
+def test_c5_band_production_vs_oracle(gpu_ctx, oracle_mod, monkeypatch):
+    """C5 rows 524..555 (the middle of the frame, through the curve cloud),
+    passes 252..255 of the 256-spp frame: 4 chunks of one pass (61 440 paths,
+    above the tail threshold) on 2 lanes."""
+    import torch
+    nx, ny, y0, rows, s0, n = 1920, 1080, 524, 32, 252, 4
+    sc = scenes.cornell_curves(nx, ny)
+    _env(monkeypatch, RTAMD_MAX_PATHS=rows * nx, RTAMD_LANES=2)
+    acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    h = gpu.render_rows_device(sc, nx, ny, y0, rows, s0, n, SEED, acc.data_ptr())
+    st = gpu.stats(h)
+    got = acc.cpu().numpy()
+    assert st.chunks >= 4 and st.lanes == 2, (st.chunks, st.lanes)
+    assert st.extend_rays > st.paths and st.finish_paths > 0
+    assert st.curve_pooled_batches > 0
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    ref = np.zeros(nx * ny * 3)
+    o = oracle_mod.build_scene(sc)
+    _, segs = o.render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=host_threads())
+    rms, dmax, nbad, npx = _compare(got[3 * lo:3 * hi], ref[3 * lo:3 * hi], n)
+    print("C5 band rows %d..%d passes %d..%d: rms=%.3e max=%.3e pixels>1e-9: %d/%d segments gpu %d oracle %d "
+          "chunks=%d lanes=%d pooled batches=%d"
+          % (y0, y0 + rows - 1, s0, s0 + n - 1, rms, dmax, nbad, npx, st.segments, segs, st.chunks, st.lanes,
+             st.curve_pooled_batches))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)
+    assert not got[:3 * lo].any() and not got[3 * hi:].any()
+
+
+def _flat_curve_scene(nx, ny):
+    """The Cornell frame with 20 000 short curves (extent ~0.5, width 3) in
+    front of the camera: half straight (l0 is rounding only, converge's depth
+    estimate ~ -20), half bent by ~1e-3 (depth -2..-4): every root is a leaf.
+    Sparse enough that paths are short: in a denser cloud (200 000 curves of
+    width 6) ribbons graze each other so often that the 1-ulp differences of
+    OCML's sin / cos from glibc's flip whole paths (a 1-ulp change of every
+    oracle cos alone changes 0.7 % of that scene's pixels)."""
+    rs = np.random.default_rng(0x5EED0105)
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(4, 4, 4)))
+    m = 20000
+    base = rs.uniform(150.0, 400.0, size=(m, 1, 3))
+    t = np.linspace(0.0, 0.5, 4).reshape(1, 4, 1) * rs.normal(size=(m, 1, 3))
+    bend = 1e-3 * rs.normal(size=(m, 4, 3))
+    bend[: m // 2] = 0.0
+    objs = [g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, white)),
+            g.make_yz_rect(0, 555, 0, 555, 0, red),
+            g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)),
+            g.make_xz_rect(0, 555, 0, 555, 0, white),
+            g.make_bvh_node([g.bezier_array((base + t + bend).reshape(m, 12), 3.0, white)], 0, 0)]
+    return g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
+
+
+def test_flat_curves_in_pooled_batches_vs_oracle(gpu_ctx, oracle_mod, monkeypatch):
+    """Flat curves reach the pooled stage B of k_extend_curves (counted on the
+    device), the render raises no fault, and the image matches the oracle."""
+    nx, ny, spp = 128, 128, 16          # a flipped sample moves its pixel by ~1e-2 / spp
+    sc = _flat_curve_scene(nx, ny)
+    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=1)
+    acc = np.zeros(nx * ny * 3)
+    h = gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
+    st = gpu.stats(h)
+    print("flat curves: pooled batches %d, flat survivors walked in them %d, segments %d"
+          % (st.curve_pooled_batches, st.curve_flat_pooled, st.segments))
+    assert st.finish_paths == 0
+    assert st.curve_pooled_batches > 0 and st.curve_flat_pooled > 0
+    ref, _ = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=host_threads())
+    rms, dmax, nbad, npx = _compare(acc, ref, spp)
+    print("flat curves vs oracle: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)
+    # the same render through the tail kernel's per-lane curve test: bit for bit
+    monkeypatch.delenv("RTAMD_TAIL_PATHS")
+    monkeypatch.delenv("RTAMD_TAIL_DIV")
+    monkeypatch.setenv("RTAMD_TAIL_PATHS", "100000000")
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, spp, SEED, b)
+    assert np.array_equal(acc, b)
+
+
+@pytest.mark.parametrize("wavefront", [False, True])
+def test_curve_deeper_than_walk_faults(gpu_ctx, monkeypatch, wavefront):
+    """A curve of width 1e-13 spanning ~150 units needs ~27 subdivision levels
+    (bezier.scm:180-193); the walk supports 24, so the render fails with the
+    curve fault instead of a silently clamped image, and the next render of a
+    normal scene is unaffected."""
+    if wavefront:
+        _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000)
+    nx, ny, spp = 48, 48, 1
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    curve = g.make_bezier(v.vec3(200, 200, 250), v.vec3(260, 380, 260), v.vec3(320, 150, 280), v.vec3(370, 330, 300),
+                          1e-13, white)
+    sc = g.make_scene([g.make_xz_rect(0, 555, 0, 555, 0, white), curve], scenes.cornell_camera_for(nx, ny),
+                      g.sky_color)
+    acc = np.zeros(nx * ny * 3)
+    with pytest.raises(RtError, match="curve walk"):
+        gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
+    ok = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.cornell_bezier(nx, ny), nx, ny, 0, spp, SEED, ok)
+    assert np.isfinite(ok).all()

@@ -4,7 +4,8 @@ interleaved tiles with librtamd (rt_render_shard_device, compact accumulator)
 through rtamd.dist.render_frame — bench.py's per-step call — and rank 0's
 gathered frame must equal a one-process rt_render_device frame bit for bit.
 Only the transport differs from the 8-GPU bench (gloo through host memory
-instead of RCCL over xGMI)."""
+instead of RCCL over xGMI); the RCCL path itself runs at world size 1
+(test_rccl_gather_world1_equals_render_device)."""
 import os
 import socket
 
@@ -64,6 +65,56 @@ def test_multiprocess_tile_shards_equal_one_process_frame(gpu_ctx, tmp_path, mon
     if wavefront:
         monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
         monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    full = torch.zeros(NX * NY * 3, dtype=torch.float64, device="cuda")
+    gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(np.load(out), full.cpu().numpy())
+
+
+def _nccl_worker(rank, world, port, out_path):
+    """RCCL ("nccl" backend) at world size 1 on cuda:0 — the only RCCL
+    configuration a one-GPU box can run: the rank renders its (only) shard
+    into a compact device accumulator and rtamd.dist.gather_frame moves it
+    with dist.gather over RCCL into a device frame, twice (the second frame
+    reuses the cached exchange buffers)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "scheme-raytrace_amd"))
+    import torch
+    import torch.distributed as dist
+
+    from rtamd import dist as rdist
+    from rtamd import gpu, scenes
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    scene = scenes.random_scene(NX, NY)
+    ctx = gpu.default_context(0)
+    local = torch.zeros(rdist.local_size(NX, NY, rank, world), dtype=torch.float64, device="cuda")
+    frame = torch.full((NX * NY * 3,), -1.0, dtype=torch.float64, device="cuda")
+    frames = []
+    for _ in range(2):
+        local.zero_()
+        gpu.render_shard_device(scene, NX, NY, 0, SPP, SEED, rank, world, local.data_ptr(),
+                                stream=torch.cuda.current_stream().cuda_stream, ctx=ctx)
+        out = rdist.gather_frame(local, NX, NY, rank, world, out=frame)
+        assert out is frame and out.device.type == "cuda"
+        frames.append(out.cpu().numpy().copy())
+    torch.cuda.synchronize()
+    assert np.array_equal(frames[0], frames[1])
+    np.save(out_path, frames[0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_world1_equals_render_device(gpu_ctx, tmp_path):
+    import torch
+    from rtamd import gpu, scenes
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_nccl_worker, args=(1, _free_port(), out), nprocs=1, join=True)
     full = torch.zeros(NX * NY * 3, dtype=torch.float64, device="cuda")
     gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
     torch.cuda.synchronize()

@@ -12,7 +12,9 @@ import os
 import numpy as np
 import pytest
 
+from conftest import host_threads
 from rtamd import gpu, scenes
+from rtamd._lib import RtError
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +35,7 @@ def _both(scene, nx, ny, spp, oracle_mod, spp_begin=0, seed=SEED):
     acc = np.zeros(nx * ny * 3)
     gpu.render_host(scene, nx, ny, spp_begin, spp, seed, acc)
     o = oracle_mod.build_scene(scene)
-    ref, _ = o.render(nx, ny, spp_begin, spp, seed, nthreads=os.cpu_count() or 1)
+    ref, _ = o.render(nx, ny, spp_begin, spp, seed, nthreads=host_threads())
     return acc, ref
 
 
@@ -71,7 +73,7 @@ def test_full_width_band_parity(gpu_ctx, oracle_mod):
     o = oracle_mod.build_scene(scene)
     lo, hi = 500 * nx, 508 * nx          # rows 500..507 (horizon region)
     ref = np.zeros(nx * ny * 3)
-    o.render(nx, ny, 0, spp, SEED, ref, lo, hi, nthreads=os.cpu_count() or 1)
+    o.render(nx, ny, 0, spp, SEED, ref, lo, hi, nthreads=host_threads())
     rms, dmax, nbad, npx = _compare(acc[3 * lo:3 * hi], ref[3 * lo:3 * hi], spp)
     print("band: rms=%.3e max=%.3e bad=%d/%d" % (rms, dmax, nbad, npx))
     assert rms <= RMS_TOL
@@ -371,24 +373,6 @@ def test_curve_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
-def test_curves_c5_scale(gpu_ctx, oracle_mod):
-    """Config C5's scene (2^20 curves in a BVH) at 1920x1080: a band of
-    pixels against the oracle.  The oracle walks the curves as a flat list,
-    so only a few pixels are checked, at 1 spp, on the rows where the band
-    meets the curve cloud."""
-    nx, ny = 1920, 1080
-    sc = scenes.cornell_curves(nx, ny)
-    acc = np.zeros(nx * ny * 3)
-    gpu.render_host(sc, nx, ny, 0, 1, SEED, acc)
-    assert np.isfinite(acc).all()
-    o = oracle_mod.build_scene(sc)
-    pix = np.array([540 * nx + x for x in range(900, 1020, 15)], dtype=np.uint32)
-    ref = np.zeros(nx * ny * 3)
-    o.render_pixels(nx, ny, 0, 1, SEED, ref, pix, nthreads=os.cpu_count() or 1)
-    for j in pix:
-        assert np.abs(acc[3 * j:3 * j + 3] - ref[3 * j:3 * j + 3]).max() <= 1e-9, j
-
-
 def test_media_in_list_order(gpu_ctx, oracle_mod):
     """A medium listed between other objects (and a sphere-bounded one, and
     one under an instance) draws its random number with the closest hit of
@@ -533,3 +517,49 @@ def test_curve_kernels_bitwise(gpu_ctx, monkeypatch, flat_curves):
     assert np.isfinite(imgs[0]).all()
     for a in imgs[1:]:
         assert np.array_equal(imgs[0], a), np.abs(imgs[0] - a).max()
+
+
+@pytest.mark.parametrize("name", ["cover", "cornell", "test_bezier", "cornell_bezier", "curves_small", "cornell_klein",
+                                  "bvh_sah"])
+def test_hit_rays_vs_oracle_hit_world(gpu_ctx, oracle_mod, name):
+    """rt_hit_rays (the extend kernels' closest_hit on a caller's rays) against
+    the oracle's hit-obj-list over the same scene list (orc_hit_world): camera
+    and scattered-like rays, unit and raw directions, |dir| < 1, times 0 and
+    inside the shutter.  Same t bit for bit and the same material."""
+    nx, ny = 64, 36
+    sc = scenes.SCENES[name](nx, ny)
+    o = oracle_mod.build_scene(sc)
+    rng = np.random.default_rng(0x5EED0201)
+    cam = np.array(sc.camera.slots())
+    n = 4096
+    # camera rays through random film points, then rays from random points inside the scene's box
+    s_, t_ = rng.uniform(0, 1, n // 2), rng.uniform(0, 1, n // 2)
+    d0 = cam[0:3] + s_[:, None] * cam[3:6] + t_[:, None] * cam[6:9] - cam[9:12]
+    o0 = np.broadcast_to(cam[9:12], d0.shape)
+    tm0 = cam[22] + rng.uniform(0, 1, n // 2) * (cam[23] - cam[22])
+    lo, hi = (np.array([0.0, 0.0, 0.0]), np.array([555.0, 555.0, 555.0])) if "cornell" in name else \
+        (np.array([-6.0, 0.0, -4.0]), np.array([10.0, 3.0, 10.0]))
+    o1 = rng.uniform(lo, hi, (n // 2, 3))
+    d1 = rng.normal(size=(n // 2, 3))
+    d1[::3] /= np.linalg.norm(d1[::3], axis=1)[:, None]
+    d1[1::3] *= 0.3
+    rays = np.zeros((n, 7))
+    rays[:n // 2, 0:3], rays[:n // 2, 3:6], rays[:n // 2, 6] = o0, d0, tm0
+    rays[n // 2:, 0:3], rays[n // 2:, 3:6] = o1, d1
+    t, m = gpu.hit_rays(sc, rays)
+    bad = []
+    hits = 0
+    for k in range(n):
+        h = o.hit_world(rays[k, 0:3], rays[k, 3:6], rays[k, 6])
+        et, em = (h[0], int(h[7])) if h else (0.0, -1)
+        hits += h is not None
+        if et != t[k] or em != m[k]:
+            bad.append((k, et, em, t[k], m[k]))
+    print("%s: %d rays, %d hits, %d differ" % (name, n, hits, len(bad)), bad[:3])
+    assert hits > n // 8
+    assert len(bad) <= n // 1000, bad[:5]
+
+
+def test_hit_rays_refuses_media(gpu_ctx):
+    with pytest.raises(RtError, match="media"):
+        gpu.hit_rays(scenes.cornell_smoke(16, 16), np.zeros((1, 7)))

@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+from conftest import host_threads
 from rtamd import gpu, scenes
 
 pytestmark = pytest.mark.gpu
@@ -57,7 +58,7 @@ def c2_band(gpu_ctx, oracle_mod):
                 os.environ[k] = v
     ref = np.zeros(nx * ny * 3)
     lo, hi = y0 * nx, (y0 + rows) * nx
-    oracle_mod.build_scene(scene).render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=os.cpu_count() or 1)
+    oracle_mod.build_scene(scene).render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=host_threads())
     return dict(nx=nx, ny=ny, y0=y0, rows=rows, s0=s0, n=n, scene=scene, got=got, ref=ref, stats=st, lo=lo, hi=hi)
 
 
@@ -196,7 +197,7 @@ def test_noise_texture_vs_oracle(gpu_ctx, oracle_mod, monkeypatch, wavefront):
     sc = _noise_scene(nx, ny)
     acc = np.zeros(nx * ny * 3)
     gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
-    ref, _ = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=os.cpu_count() or 1)
+    ref, _ = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=host_threads())
     rms, dmax, nbad, npx = _compare(acc, ref, spp)
     print("noise texture (wavefront=%s): rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (wavefront, rms, dmax, nbad, npx))
     assert np.isfinite(acc).all() and acc.sum() > 0
@@ -231,3 +232,44 @@ def test_sampler_cap_raises_fault_not_hang(gpu_ctx, monkeypatch, wavefront):
     gpu.render_device(scene, nx, ny, 0, spp, SEED, acc.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(acc, good)
+
+
+def test_pools_shared_per_context_and_released(gpu_ctx, monkeypatch):
+    """The render lanes' path pools belong to the context: two scenes render
+    on one context in turn, rt_context_release_pools frees the pools, and the
+    next renders (pools allocated again) are bit for bit the same."""
+    import torch
+    from rtamd.gpu import Context
+    ctx = Context(0)
+    try:
+        nx, ny, spp = 96, 54, 8
+        a, b = scenes.random_scene(nx, ny), scenes.cornell_box(nx, ny)
+        outs = []
+        for _ in range(2):
+            for sc in (a, b):
+                acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+                gpu.render_device(sc, nx, ny, 0, spp, SEED, acc.data_ptr(), ctx=ctx)
+                torch.cuda.synchronize()
+                outs.append(acc.cpu().numpy())
+            ctx.release_pools()
+        assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[1], outs[3])
+        assert not np.array_equal(outs[0], outs[1])
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("switch", ["RTAMD_NO_EXTEND_LDS", "RTAMD_NO_CAMERA_LDS", "RTAMD_FINISH_GENERIC"])
+def test_kernel_variants_bitwise(gpu_ctx, monkeypatch, switch):
+    """The cover scene's specialised kernels (k_extend_lds, k_camera, the SOLO
+    tail) against the general ones (k_extend<F>, k_raygen + k_extend, the
+    group-loop tail): the same image bit for bit."""
+    nx, ny, spp = 64, 36, 3
+    if switch != "RTAMD_FINISH_GENERIC":
+        _wavefront_only(monkeypatch)
+    a = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.random_scene(nx, ny), nx, ny, 0, spp, SEED, a)
+    monkeypatch.setenv(switch, "1")
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(scenes.random_scene(nx, ny), nx, ny, 0, spp, SEED, b)
+    assert np.isfinite(a).all()
+    assert np.array_equal(a, b)

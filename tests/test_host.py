@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_errors_without_gpu():
     L = _lib.lib()
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == 4
     h = ctypes.c_int(0)
     assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
     assert b"invalid context" in L.rt_last_error()
@@ -187,7 +187,7 @@ def test_c_example_builds_against_the_abi(tmp_path):
     import subprocess
     exe = _build_c_example(tmp_path)
     out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
-    assert out.strip() == "rt_abi_version 3"
+    assert out.strip() == "rt_abi_version 4"
 
 
 def test_load_points_and_points_to_bezier(tmp_path):
