@@ -169,8 +169,9 @@ def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
     o = oracle.build_scene(scene)
     y0, rows = band_rows(ny)
     lo, hi = y0 * nx, (y0 + rows) * nx
-    # calibrate: one pass over 8 rows
+    # calibrate: one pass over 8 rows (after a zero-pixel call that builds the oracle's trees)
     cal = np.zeros(nx * ny * 3)
+    o.render(nx, ny, spp - 1, 1, seed, cal, lo, lo, T)
     t = time.perf_counter()
     o.render(nx, ny, spp - 1, 1, seed, cal, lo, min(hi, lo + 8 * nx), T)
     per_row_pass = (time.perf_counter() - t) / min(8, rows)
