@@ -683,6 +683,7 @@ int commit_scene(Scene* s, int world) {
             } else {
                 li.local = (int)bez.size();
                 bez.push_back(bezier_rec(o));
+                bez.back().order = (uint32_t)r.leaf;          // the flattened list position
                 lbez.push_back(li);
             }
         }
@@ -778,6 +779,11 @@ int commit_scene(Scene* s, int world) {
         } else if (L.type == LEAF_BEZIER) {
             li->local = (int)bez.size(); lbez.push_back(*li);
             bez.push_back(bezier_rec(o));
+            {   // the flattened list position (medium boundaries come from f.bounds: order 0, ties irrelevant)
+                const uintptr_t p = reinterpret_cast<uintptr_t>(&L), b0 = reinterpret_cast<uintptr_t>(f.leaves.data());
+                const bool in_list = p >= b0 && p < b0 + f.leaves.size() * sizeof(LeafTmp);
+                bez.back().order = in_list ? (uint32_t)((p - b0) / sizeof(LeafTmp)) : 0u;
+            }
         } else if (L.type == LEAF_KLEIN) {
             li->local = (int)klein.size(); lklein.push_back(*li);
             klein.push_back({o.c0[0], o.c0[1], o.c0[2], 0.0});

@@ -51,7 +51,8 @@ struct alignas(32) MSphereRec {                                        // center
 struct alignas(64) RectRec { double a0, a1, b0, b1, k, pad0, pad1, pad2; };
 // Cubic Bezier curve of a given width (bezier.scm:61-66): control points,
 // width1 = width/2, width2 = width1^2, eps8 = 8*(width/20).
-struct alignas(64) BezierRec { double cp[12]; double w1, w2, eps8, pad; };
+// order: the curve's position in the flattened object list (ties between curves at one z go to the later one)
+struct alignas(64) BezierRec { double cp[12]; double w1, w2, eps8; uint32_t order, pad; };
 constexpr int kBezMaxDepth = 24;               // subdivision levels the curve test supports
 // Constant medium (geometry.scm:545-578): its boundary is the closest hit over
 // the boundary groups [bg_begin, bg_end) of DevScene::bgroups; neg_inv_density

@@ -309,68 +309,105 @@ __device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay
     return !bez_culled(c, B.w1, tmax);
 }
 
-// Returns true and the curve's t if it reports a hit for t-max `tmax`.
+// The subdivision walk of converge (bezier.scm:121-175) as a per-lane state
+// machine: one node per step, so the batched curve kernels (stage B) can hand
+// a lane whose curve is finished the next survivor while the others keep
+// walking; bezier_test runs it to the end.
 //
 // The answer does not depend on the order of the recursion: a leaf hit at
 // z <= tmax lies on its sub-curve, inside every ancestor's box, so no
 // ancestor culls it and converge's result is min z over all leaf hits with
-// z <= tmax.  The walk below therefore also culls with the best z found so
-// far (it cannot hide a smaller z), which only removes work.
-__device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
-    const double w1 = B.w1, w2 = B.w2;
-    Bez4 c;
-    bez_load(B, R, c);
-    if (bez_culled(c, w1, tmax)) return false;
-    // flatness -> subdivision depth (:180-193)
+// z <= tmax.  The walk therefore also culls with the best z found so far (it
+// cannot hide a smaller z, and culling only gets stronger as the best z
+// drops), which only removes work.
+//
+// Depth-first, without a stack: node (L, idx) is the sub-curve reached from
+// the root by L splits at 0.5 taking the halves given by idx's bits (MSB
+// first); its parameter range is [idx, idx + 1] * 2^-L.  A split culls both
+// halves at once: the walk goes into the left half if it survives, else
+// straight into the right one (already in registers), and remembers in rmask
+// whether a left half's right sibling survived.  Only a right sibling that
+// survived next to a surviving left half is revisited later, re-derived from
+// the root by the same split sequence, so every sub-curve carries the exact
+// values the reference's recursion computes.  (Keeping the deepest pending
+// right half in registers instead cut the re-derivation splits per curve from
+// 15 to 5 at C5, but the persistent curve kernel then spills: 120.6 vs 137.8
+// Mrays/s at 4 spp.)
+struct BezWalk {
+    Bez4 root, c;
+    double best, tmax, w1, w2;
+    int L, leaf_level, base;        // base: the level the walk started at (a donated subtree's root; else 0)
+    uint32_t idx, it, cap;
+    uint32_t rmask;                 // bit L: the right sibling of the level-L left half was culled at the split
+    bool fresh, found;              // fresh: c is valid and passed the cull
+};
+// converge's subdivision depth from the transformed curve's flatness (:180-193)
+__device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
     double l0 = -kTmax;
-    {
-        const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
-        l0 = fmax(fmax(x0, y0), l0);
-        const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
-        l0 = fmax(fmax(x1, y1), l0);
-    }
-    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / B.eps8) / log(4.0);
-    const int maxd = (md == -INFINITY) ? 0 : (int)ceil(md);
-    // converge has no depth limit (bezier.scm:189-193); a curve needing more
-    // levels than the walk's 32-bit node index holds fails the render loudly
-    if (!(maxd <= kBezMaxDepth)) { raise_fault(RT_FAULT_CURVE); return false; }
-    bool found = false;
-    double best = tmax;
-    // Depth-first walk of the subdivision tree without a stack: node (L, idx)
-    // is the sub-curve reached from the root by L splits at 0.5 taking the
-    // halves given by idx's bits (MSB first); its parameter range is
-    // [idx, idx + 1] * 2^-L.  Moving to a right sibling re-derives the node by
-    // the same split sequence from the root, so every sub-curve carries the
-    // exact values the reference's recursion computes.
-    const Bez4 root = c;
-    // converge's depth < 0 (root level has depth maxd); a negative maxd (a flat
-    // curve) makes the root a leaf, as a leaf level of 0 does
-    const int leaf_level = maxd + 1 > 0 ? maxd + 1 : 0;
-    int L = 0;
-    uint32_t idx = 0;
-    bool fresh = true;
-    // the walk visits each of the <= 2^(leaf_level+1) subdivision nodes at most once
-    const uint32_t cap = 4u << leaf_level;
-    for (uint32_t it = 0;; ++it) {
-        if (it > cap) { raise_fault(RT_FAULT_CURVE); break; }
-        if (!fresh) {
-            c = root;
-            for (int k = L - 1; k >= 0; --k) {
-                Bez4 l, r;
-                bez_split(c, l, r);
-                c = ((idx >> k) & 1u) ? r : l;
-            }
+    const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
+    l0 = fmax(fmax(x0, y0), l0);
+    const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
+    l0 = fmax(fmax(x1, y1), l0);
+    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / eps8) / log(4.0);
+    // saturates at kBezMaxDepth + 1: the caller faults on anything deeper than the walk supports
+    return (md == -INFINITY) ? 0 : (md > (double)(kBezMaxDepth + 1) ? kBezMaxDepth + 1 : (int)ceil(md));
+}
+// set up the walk of root-transformed curve `root` for t-max tmax (the root
+// has passed the cull) down to leaf level leaf_level = max(0, maxd + 1): a
+// negative maxd (a flat curve) makes the root a leaf (:130, 189-193)
+__device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, const double w1, const double w2,
+                                              const double tmax, const int leaf_level) {
+    s.root = root; s.c = root;
+    s.w1 = w1; s.w2 = w2; s.tmax = tmax;
+    s.leaf_level = leaf_level;
+    s.cap = 4u << s.leaf_level;              // each of the <= 2^(leaf_level+1) nodes is visited at most once
+    s.L = 0; s.base = 0; s.idx = 0; s.it = 0; s.rmask = 0;
+    s.fresh = true; s.found = false; s.best = tmax;
+}
+// set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
+// stage A's root cull) is given; false if the whole curve is culled
+__device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
+                                               const int leaf_level) {
+    Bez4 root;
+    bez_load(B, R, root);
+    if (bez_culled(root, B.w1, tmax)) return false;
+    bez_walk_init(s, root, B.w1, B.w2, tmax, leaf_level);
+    return true;
+}
+// one node of the walk; true once the walk is over
+__device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
+    if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
+    bool live = true;
+    if (!s.fresh) {                                             // a right sibling that survived its split
+        s.c = s.root;
+        for (int k = s.L - 1; k >= 0; --k) {
+            Bez4 l, r;
+            bez_split(s.c, l, r);
+            s.c = ((s.idx >> k) & 1u) ? r : l;
         }
-        fresh = false;
-        if (!bez_culled(c, w1, best)) {
-            if (L < leaf_level) {                               // split, left first (:167-175)
-                Bez4 l, r;
-                bez_split(c, l, r);
-                c = l; ++L; idx <<= 1; fresh = true;
-                continue;
+        live = !bez_culled(s.c, s.w1, s.best);                  // (:123-128) with the best z so far
+    }
+    s.fresh = false;
+    if (live) {
+        const Bez4& c = s.c;
+        if (s.L < s.leaf_level) {                               // split, left first (:167-175)
+            Bez4 l, r;
+            bez_split(c, l, r);
+            const bool kl = !bez_culled(l, s.w1, s.best), kr = !bez_culled(r, s.w1, s.best);
+            if (kl || kr) {
+                ++s.L;
+                if (kl) {
+                    s.c = l; s.idx <<= 1;
+                    s.rmask = kr ? (s.rmask & ~(1u << s.L)) : (s.rmask | (1u << s.L));
+                } else {
+                    s.c = r; s.idx = (s.idx << 1) | 1u;
+                }
+                s.fresh = true;
+                return false;
             }
+        } else {
             // leaf segment (:130-166)
-            const double v0 = ldexp((double)idx, -L), vn = v0 + ldexp(1.0, -L);
+            const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
             const v3 dir = c.p3 - c.p0;
             v3 dp0 = bez_tan(c, false);
             if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
@@ -384,104 +421,64 @@ __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R,
                         w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
                         const double v = v0 * (1.0 - w) + vn * w;
                         const v3 p = bez_point(c, v);             // sub-curve at the global v (Q11)
-                        if (!(p.x * p.x + p.y * p.y >= w2 || p.z <= 0.0001 || tmax < p.z)) {
-                            if (!found || p.z < best) best = p.z;
-                            found = true;
+                        if (!(p.x * p.x + p.y * p.y >= s.w2 || p.z <= 0.0001 || s.tmax < p.z)) {
+                            if (!s.found || p.z < s.best) s.best = p.z;
+                            s.found = true;
                         }
                     }
                 }
             }
         }
-        while (L > 0 && (idx & 1u)) { --L; idx >>= 1; }          // climb past right children
-        if (L == 0) break;
-        ++idx;                                                  // right sibling
     }
-    if (!(found && kTmin < best)) return false;                 // :201
-    tout = best;
-    return true;
+    // climb past right halves and past left halves whose right sibling was culled at the split
+    while (s.L > s.base && ((s.idx & 1u) || ((s.rmask >> s.L) & 1u))) { --s.L; s.idx >>= 1; }
+    if (s.L == s.base) return true;
+    ++s.idx;                                                    // the surviving right sibling
+    return false;
 }
 
-// The walk of bezier_test as a per-lane state machine (stage B of the batched
-// curve tests): one node per call, so a lane whose curve is finished can take
-// the next survivor while the others keep walking.  Same nodes, same order,
-// same arithmetic as bezier_test.
-struct BezWalk {
-    Bez4 root, c;
-    double best, tmax, w1, w2;
-    int L, leaf_level;
-    uint32_t idx, it, cap;
-    bool fresh, found;
-};
-// converge's subdivision depth from the transformed curve's flatness (:180-193)
-__device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
-    double l0 = -kTmax;
-    const double x0 = fabs((c.p0.x + -2.0 * c.p1.x) + c.p2.x), y0 = fabs((c.p0.y + -2.0 * c.p1.y) + c.p2.y);
-    l0 = fmax(fmax(x0, y0), l0);
-    const double x1 = fabs((c.p1.x + -2.0 * c.p2.x) + c.p3.x), y1 = fabs((c.p1.y + -2.0 * c.p2.y) + c.p3.y);
-    l0 = fmax(fmax(x1, y1), l0);
-    const double md = log((((1.4142135623730951 * 4.0) * 3.0) * l0) / eps8) / log(4.0);
-    // saturates at kBezMaxDepth + 1: the caller faults on anything deeper than the walk supports
-    return (md == -INFINITY) ? 0 : (md > (double)(kBezMaxDepth + 1) ? kBezMaxDepth + 1 : (int)ceil(md));
+// Work sharing: the right siblings still pending on a walk's path (levels
+// base+1 .. L whose path node is a left half whose right sibling survived its
+// split), as a bit mask by level.
+__device__ __forceinline__ uint32_t bez_walk_pending(const BezWalk& s) {
+    uint32_t pend = 0;
+    for (int l = s.base + 1; l <= s.L; ++l)
+        if (!((s.idx >> (s.L - l)) & 1u) && !((s.rmask >> l) & 1u)) pend |= 1u << l;
+    return pend;
 }
-// set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
-// stage A's root cull) is given; false if the whole curve is culled
-__device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
-                                               const int leaf_level) {
-    bez_load(B, R, s.root);
-    s.w1 = B.w1; s.w2 = B.w2; s.tmax = tmax;
-    if (bez_culled(s.root, s.w1, tmax)) return false;
-    s.leaf_level = leaf_level;
-    s.cap = 4u << s.leaf_level;
-    s.c = s.root; s.L = 0; s.idx = 0; s.it = 0; s.fresh = true; s.found = false; s.best = tmax;
+// Hand the shallowest pending right sibling to another lane: returns its
+// (level, index); this walk will skip it.
+__device__ __forceinline__ void bez_walk_donate(BezWalk& s, const uint32_t pend, uint32_t& l, uint32_t& ridx) {
+    l = (uint32_t)__builtin_ctz(pend);
+    ridx = (s.idx >> ((uint32_t)s.L - l)) | 1u;
+    s.rmask |= 1u << l;
+}
+// Start a walk of the donated subtree rooted at node (l, ridx) of curve B
+// (re-derived from the root at the first step; the walk ends back at level l).
+__device__ __forceinline__ void bez_walk_take(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
+                                              const int leaf_level, const uint32_t l, const uint32_t ridx) {
+    Bez4 root;
+    bez_load(B, R, root);
+    bez_walk_init(s, root, B.w1, B.w2, tmax, leaf_level);
+    s.L = (int)l; s.base = (int)l; s.idx = ridx; s.fresh = false;
+}
+
+// Returns true and the curve's t if it reports a hit for t-max `tmax`
+// (bezier.scm:176-214): the root cull, the depth estimate, then the walk.
+__device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
+    Bez4 c;
+    bez_load(B, R, c);
+    if (bez_culled(c, B.w1, tmax)) return false;
+    const int maxd = bez_maxd(c, B.eps8);
+    // converge has no depth limit (bezier.scm:189-193); a curve needing more
+    // levels than the walk's 32-bit node index holds fails the render loudly
+    if (maxd > kBezMaxDepth) { raise_fault(RT_FAULT_CURVE); return false; }
+    BezWalk wk;
+    bez_walk_init(wk, c, B.w1, B.w2, tmax, maxd + 1 > 0 ? maxd + 1 : 0);
+    while (!bez_walk_step(wk)) {}
+    if (!(wk.found && kTmin < wk.best)) return false;           // :201
+    tout = wk.best;
     return true;
-}
-// one node of the walk; true once the walk is over
-__device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
-    if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
-    if (!s.fresh) {
-        s.c = s.root;
-        for (int k = s.L - 1; k >= 0; --k) {
-            Bez4 l, r;
-            bez_split(s.c, l, r);
-            s.c = ((s.idx >> k) & 1u) ? r : l;
-        }
-    }
-    s.fresh = false;
-    const Bez4& c = s.c;
-    if (!bez_culled(c, s.w1, s.best)) {
-        if (s.L < s.leaf_level) {                               // split, left first (:167-175)
-            Bez4 l, r;
-            bez_split(c, l, r);
-            s.c = l; ++s.L; s.idx <<= 1; s.fresh = true;
-            return false;
-        }
-        // leaf segment (:130-166)
-        const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
-        const v3 dir = c.p3 - c.p0;
-        v3 dp0 = bez_tan(c, false);
-        if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
-        if (!(dot2d(dp0, c.p0 * -1.0) < 0.0)) {
-            v3 dpn = bez_tan(c, true);
-            if (dot2d(dir, dpn) < 0.0) dpn = dpn * -1.0;
-            if (!(dot2d(dpn, c.p3) < 0.0)) {
-                double w = dir.x * dir.x + dir.y * dir.y;
-                if (w != 0.0) {
-                    w = (c.p0.x * dir.x + c.p0.y * dir.y) / (-w);
-                    w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
-                    const double v = v0 * (1.0 - w) + vn * w;
-                    const v3 p = bez_point(c, v);                 // sub-curve at the global v (Q11)
-                    if (!(p.x * p.x + p.y * p.y >= s.w2 || p.z <= 0.0001 || s.tmax < p.z)) {
-                        if (!s.found || p.z < s.best) s.best = p.z;
-                        s.found = true;
-                    }
-                }
-            }
-        }
-    }
-    while (s.L > 0 && (s.idx & 1u)) { --s.L; s.idx >>= 1; }   // climb past right children
-    if (s.L == 0) return true;
-    ++s.idx;                                                    // right sibling
-    return false;
 }
 
 #ifdef RT_STATS
@@ -491,7 +488,7 @@ __device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
 // [16..26] time-0 tree; curve trees: [11] rays, [12] node visits, [13] leaf
 // visits, [14] queued curve candidates, [15] root-cull survivors, [27] flushes,
 // [28] wave loop iterations, [29] waves, [30] lanes
-__device__ unsigned long long g_stats[32];
+__device__ unsigned long long g_stats[48];
 #define RT_STAT(k, v) atomicAdd(&g_stats[k], (unsigned long long)(v))
 #else
 #define RT_STAT(k, v) ((void)0)
@@ -504,7 +501,9 @@ __device__ unsigned long long g_stats[32];
 // owner lane) candidates to a wave-local LDS queue; when 64 have gathered the
 // wave tests them together: first the cheap root cull for every candidate,
 // then the full subdivision for the survivors only, each lane taking one
-// pair.  Per owner the smallest z wins (ties: smallest curve index).  A
+// pair.  Per owner the smallest z wins; on a tie the later curve of the list
+// (BezierRec::order), as hit-obj-list's scan reports a curve at
+// z <= t-max (geometry.scm:41-46, bezier.scm:164) — bez_take_batch.  A
 // curve's answer does not depend on the t-max it is tested with, beyond
 // being reported only when z <= t-max (see bezier_test), so deferring the
 // tests changes no result.
@@ -518,7 +517,7 @@ struct BezWave {
     BezRay ray[64];                 // owner lane's ray-space matrix
     double cl[64];                  // owner's closest t when a batch runs
     double hz[64];                  // owner's best curve z from the batch
-    uint32_t hid[64];               // and its curve index
+    unsigned long long hkey[64];    // and its curve: list order << 32 | curve index (ties: the later curve)
     uint32_t q[kBezQ];              // candidates: curve << 6 | owner
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
@@ -572,7 +571,7 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
 }
 
 // Stage B: full subdivision of the first nb survivors, one per lane, then per
-// owner the smallest z (ties: smallest curve index) into hz / hid; the
+// owner the smallest z (ties: the later curve of the list) into hz / hkey; the
 // remaining svn - nb survivors move to the front.
 // Pooled-curve counters (rt_stats.curve_pooled_batches / curve_flat_pooled):
 // stage B passes over a full pool (>= RT_BEZ_HOLD survivors), and the
@@ -596,14 +595,33 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
     // Lanes take survivors one after the other from a wave-uniform cursor and
     // walk them a node per iteration (BezWalk): when at least kBezRefill
     // lanes are idle they take the next survivors together, so a lane is not
-    // held by the longest walk of a fixed batch of 64.
+    // held by the longest walk of a fixed batch of 64.  Once the survivors are
+    // all taken, idle lanes take pending right siblings (subtrees) from the
+    // lanes still walking.  A survivor's z is the minimum over every lane
+    // that walked part of it (atomicMin on the bits of the positive doubles),
+    // then converge's (< t-min t) check (:201).
     {
         BezWalk wk;
         bool busy = false;
         uint32_t si = 0, cursor = 0;
+#ifdef RT_STATS
+        // [31] passes [32] wave iterations [33] busy lane-iterations [34] walk steps [35] re-derived
+        // nodes [36] re-derivation splits [37] leaf tests [38] survivors [39] stage B clock (lane 0)
+        uint32_t n_it = 0, n_busy = 0, n_step = 0, n_red = 0, n_rsplit = 0, n_leaf = 0;
+        const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
+#endif
         const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * ((4ull << (kBezMaxDepth + 1)) + 2ull);
         for (unsigned long long g = 0;; ++g) {                    // wave-uniform
             if (g > guard_cap) { raise_fault(RT_FAULT_CURVE); break; }
+#ifdef RT_STATS
+            ++n_it;
+            n_busy += busy ? 1u : 0u;
+            if (busy) {
+                ++n_step;
+                if (!wk.fresh) { ++n_red; n_rsplit += (uint32_t)wk.L; }
+                if (wk.L >= wk.leaf_level) ++n_leaf;
+            }
+#endif
             const unsigned long long idle = __ballot(!busy);
             if (cursor < nb && (__popcll(idle) >= kBezRefill || idle == act)) {
                 if (!busy) {
@@ -611,25 +629,57 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (i < nb) {
                         const uint32_t e = W.sv[i];
                         si = i;
+                        W.sz[i] = INFINITY;
                         busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
-                        if (!busy) W.sz[i] = INFINITY;            // culled at the root
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
+            } else if (cursor >= nb && idle != 0ull && idle != act) {
+                // donation round: the candidate queue is empty during stage B, W.q carries the handover
+                const uint32_t pend = busy ? bez_walk_pending(wk) : 0u;
+                const unsigned long long dm = __ballot(pend != 0u);
+                const uint32_t nd = min((uint32_t)__popcll(dm), (uint32_t)__popcll(idle));
+                if (nd) {
+                    const uint32_t dr = lanes_below(dm);
+                    if (pend != 0u && dr < nd) {
+                        uint32_t l, ridx;
+                        bez_walk_donate(wk, pend, l, ridx);
+                        W.q[3 * dr] = si; W.q[3 * dr + 1] = l; W.q[3 * dr + 2] = ridx;
+                    }
+                    wave_sync();
+                    const uint32_t ir = lanes_below(idle);
+                    if (!busy && ir < nd) {
+                        si = W.q[3 * ir];
+                        const uint32_t e = W.sv[si];
+                        bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], W.q[3 * ir + 1],
+                                      W.q[3 * ir + 2]);
+                        busy = true;
+                    }
+                    wave_sync();
+                }
             }
             if (__ballot(busy) == 0ull) {
                 if (cursor >= nb) break;
                 continue;
             }
             if (busy && bez_walk_step(wk)) {
-                W.sz[si] = (wk.found && kTmin < wk.best) ? wk.best : INFINITY;   // :201
+                if (wk.found)
+                    atomicMin((unsigned long long*)&W.sz[si], (unsigned long long)__double_as_longlong(wk.best));
                 busy = false;
             }
         }
+#ifdef RT_STATS
+        RT_STAT(33, n_busy); RT_STAT(34, n_step); RT_STAT(35, n_red); RT_STAT(36, n_rsplit); RT_STAT(37, n_leaf);
+        if (rank == 0) {
+            RT_STAT(31, 1); RT_STAT(32, n_it); RT_STAT(38, nb);
+            RT_STAT(39, __builtin_amdgcn_s_memtime() - clk0);
+        }
+#endif
     }
     wave_sync();
     for (uint32_t base = 0; base < nb; base += nact) {
         const uint32_t i = base + rank;
+        if (i < nb && !(kTmin < W.sz[i])) W.sz[i] = INFINITY;                // :201
         if (i < nb && W.sz[i] != INFINITY)
             atomicMin((unsigned long long*)&W.hz[W.sv[i] & 63u], (unsigned long long)__double_as_longlong(W.sz[i]));
     }
@@ -638,7 +688,8 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         const uint32_t i = base + rank;
         if (i < nb && W.sz[i] != INFINITY) {
             const uint32_t e = W.sv[i], o = e & 63u;
-            if (W.sz[i] == W.hz[o]) atomicMin(&W.hid[o], e >> 6);
+            if (W.sz[i] == W.hz[o])
+                atomicMax(&W.hkey[o], ((unsigned long long)sc.bez[e >> 6].order << 32) | (e >> 6));
         }
         if (TRACK && i < nb) atomicAdd(&W.done[W.sv[i] & 63u], 1u);
     }
@@ -650,6 +701,22 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
     wave_sync();
     if (rank < rest) { W.sv[rank] = e; W.lev[rank] = lv; }
     wave_sync();
+}
+
+// The owner's result of a batch (hz, hid) against its closest hit so far: a
+// curve reports z <= the t-max it was tested with (bezier.scm:164), so it
+// takes the hit on a tie with a sphere or rect; between two curves at the
+// same z the later one of the list (BezierRec::order) is the one the scan
+// keeps, whichever batch tested it first.
+__device__ __forceinline__ void bez_take_batch(const DevScene& sc, const BezWave& W, const uint32_t lane,
+                                               const int32_t bz, double& closest, int32_t& best) {
+    const double z = W.hz[lane];
+    if (z == INFINITY || z > closest) return;
+    const uint32_t id = (uint32_t)W.hkey[lane];
+    if (z == closest && best >= bz && best < bz + sc.n_bez && sc.bez[best - bz].order > (uint32_t)(W.hkey[lane] >> 32))
+        return;
+    closest = z;
+    best = bz + (int32_t)id;
 }
 
 // Per-lane BVH traversal: every lane walks its own path through the BVH2
@@ -975,14 +1042,11 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
             const uint32_t nb = more ? svn - svn % nact : svn;
             if (nb > 0u) {
                 W.hz[lane] = INFINITY;
-                W.hid[lane] = 0xFFFFFFFFu;
+                W.hkey[lane] = 0ull;
                 wave_sync();
                 bez_stage_b(sc, W, nb, svn);
                 svn -= nb;
-                if (W.hid[lane] != 0xFFFFFFFFu && W.hz[lane] <= closest) {   // z <= the t-max it was tested with
-                    closest = W.hz[lane];
-                    best = bz + (int32_t)W.hid[lane];
-                }
+                bez_take_batch(sc, W, lane, bz, closest, best);
                 wave_sync();
             }
         }
@@ -1482,7 +1546,7 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // bvh_closest_curves; a ray finishes once its traversal has ended and every
 // curve candidate it queued has been resolved by a batch (W.done).
 // =====================================================================
-__global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const RenderParams rp,
+__global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                        const bool depth0, unsigned int* __restrict__ claim) {
@@ -1513,6 +1577,8 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
     uint32_t ray_it = 0;
 #ifdef RT_STATS
     uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
+    const unsigned long long st_clk0 = __builtin_amdgcn_s_memtime();
+    unsigned long long st_clk_a = 0;
 #endif
     for (;;) {
         // only iterations in which the lane itself works count: one waiting for a batch
@@ -1626,7 +1692,7 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
                 }
             }
         }
-        // the next node's record, in flight while the batches below run
+        // the next node's record, in flight while the batches below run (+5 % at C5)
         if (active && trav && node >= 0) N = sc.bvh2[node];
         // 4. queue this step's curve candidates (at most 2 per lane)
 #pragma unroll
@@ -1645,26 +1711,32 @@ __global__ __launch_bounds__(256) void k_extend_curves(const DevScene sc, const 
 #endif
             W.cl[lane] = closest;
             wave_sync();
+#ifdef RT_STATS
+            const unsigned long long ca = __builtin_amdgcn_s_memtime();
+#endif
             svn = bez_stage_a<true>(sc, W, qn, svn);
+#ifdef RT_STATS
+            st_clk_a += __builtin_amdgcn_s_memtime() - ca;
+#endif
             qn = 0;
             const uint32_t nb = more ? (svn >= (uint32_t)RT_BEZ_HOLD ? svn - svn % 64u : 0u) : svn;
             if (nb > 0u) {
                 W.hz[lane] = INFINITY;
-                W.hid[lane] = 0xFFFFFFFFu;
+                W.hkey[lane] = 0ull;
                 wave_sync();
                 bez_stage_b<true>(sc, W, nb, svn);
                 svn -= nb;
-                if (active && W.hid[lane] != 0xFFFFFFFFu && W.hz[lane] <= closest) {   // z <= the t-max it was tested with
-                    closest = W.hz[lane];
-                    best = bz + (int32_t)W.hid[lane];
-                }
+                if (active) bez_take_batch(sc, W, lane, bz, closest, best);
                 wave_sync();
             }
         }
     }
 #ifdef RT_STATS
     RT_STAT(20, st_steps); RT_STAT(21, st_busy); RT_STAT(22, st_wait);
-    if (lane == 0u) { RT_STAT(23, st_iter); RT_STAT(24, 1); RT_STAT(25, st_flush); }
+    if (lane == 0u) {
+        RT_STAT(23, st_iter); RT_STAT(24, 1); RT_STAT(25, st_flush);
+        RT_STAT(40, __builtin_amdgcn_s_memtime() - st_clk0); RT_STAT(41, st_clk_a);   // kernel / stage A clocks per wave
+    }
 #endif
 }
 
@@ -2649,7 +2721,7 @@ hipError_t take_curve_stats(unsigned long long out[2]) {
 extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof g_stats) != hipSuccess) return 1;
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[48] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z) != hipSuccess) return 1;
     }
     return 0;

@@ -144,3 +144,43 @@ def test_curve_deeper_than_walk_faults(gpu_ctx, monkeypatch, wavefront):
     ok = np.zeros(nx * ny * 3)
     gpu.render_host(scenes.cornell_bezier(nx, ny), nx, ny, 0, spp, SEED, ok)
     assert np.isfinite(ok).all()
+
+
+def test_duplicate_curves_tie_to_the_later_curve(gpu_ctx, oracle_mod, monkeypatch):
+    """Curves duplicated exactly (same control points, other materials) in a
+    BVH: every tie in z must go to the later curve of the list, as
+    hit-obj-list's scan keeps a curve at z <= t-max (geometry.scm:41-46,
+    bezier.scm:164).  rt_hit_rays against the oracle's hit_world, material by
+    material; the render against the oracle too."""
+    rs = np.random.default_rng(0x5EED0106)
+    mats = [g.make_lambertian(g.constant_texture(v.vec3(0.2 + 0.2 * k, 0.5, 0.3))) for k in range(3)]
+    cps = rs.uniform(100.0, 450.0, size=(300, 12))
+    objs = [g.make_xz_rect(0, 555, 0, 555, 0, mats[0]),
+            g.make_bvh_node([g.bezier_array(cps, 8.0, mats[0]), g.bezier_array(cps[::2].copy(), 8.0, mats[1]),
+                             g.bezier_array(cps[::3].copy(), 8.0, mats[2])], 0, 0)]
+    nx, ny = 48, 48
+    sc = g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
+    o = oracle_mod.build_scene(sc)
+    cam = np.array(sc.camera.slots())
+    n = 4096
+    s_, t_ = rs.uniform(0, 1, n), rs.uniform(0, 1, n)
+    rays = np.zeros((n, 7))
+    rays[:, 0:3] = cam[9:12]
+    rays[:, 3:6] = cam[0:3] + s_[:, None] * cam[3:6] + t_[:, None] * cam[6:9] - cam[9:12]
+    rays[n // 2:, 3:6] /= np.linalg.norm(rays[n // 2:, 3:6], axis=1)[:, None]   # unit directions too
+    t, m = gpu.hit_rays(sc, rays)
+    counts = np.zeros(4, dtype=int)
+    for k in range(n):
+        h = o.hit_world(rays[k, 0:3], rays[k, 3:6], 0.0)
+        et, em = (h[0], int(h[7])) if h else (0.0, -1)
+        assert (et, em) == (t[k], m[k]), (k, et, em, t[k], m[k])
+        counts[em + 1] += 1
+    print("duplicate curves: misses / floor-or-first / second / third copies hit:", counts)
+    assert counts[2] > 0 and counts[3] > 0        # ties resolved to the later copies
+    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000)
+    acc = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, 4, SEED, acc)
+    ref, _ = o.render(nx, ny, 0, 4, SEED, nthreads=host_threads())
+    rms, dmax, nbad, npx = _compare(acc, ref, 4)
+    print("duplicate curves render: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL and nbad <= max(2, npx // 200)

@@ -22,7 +22,7 @@ def main():
     spp = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     nx, ny = 1920, 1080
     lib = ctypes.CDLL(_lib.LIB_PATH)
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 48)()
     out = {}
     for mode in ("bvh0", "no_bvh0"):
         if mode == "no_bvh0":
