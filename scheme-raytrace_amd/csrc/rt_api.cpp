@@ -635,9 +635,10 @@ int commit_scene(Scene* s, int world) {
     bool tree0_direct = false;
     if (use_bvh) {
         BvhBuild bb{refs, {}};
-        // sphere trees: one primitive per leaf (measured fastest); curve trees keep 2
-        bb.leaf_max = std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; })
-                          ? 2 : 1;
+        // one primitive per leaf (measured fastest for sphere trees; for C5's curve tree, with the exact
+        // SAH sweep below 65 536 primitives, +1.5 % / +0.6 % over two per leaf: profiles/r02/ab_c5,
+        // profiles/r03/c5walk/ab_leaf1.log)
+        bb.leaf_max = 1;
         if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
         bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
                                      std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));

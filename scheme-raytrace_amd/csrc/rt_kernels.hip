@@ -2466,7 +2466,7 @@ hipError_t launch_raygen(const DevScene& sc, const RenderParams& rp, const PathS
     hipLaunchKernelGGL(k_raygen, dim3(blocks), dim3(256), 0, s, sc, rp, st);
     return hipGetLastError();
 }
-static uint32_t finish_blocks() { return 512u; }   // persistent tail grid
+static uint32_t finish_blocks() { return 512u; }    // persistent tail grid (1024: +2 % single-lane, -1 % with the two render lanes: profiles/r03/ab/ab_tail_grid.log)
 static bool finish_generic() {               // RTAMD_FINISH_GENERIC: the group-loop tail for SOLO scenes too (A/B, tests)
     const char* e = std::getenv("RTAMD_FINISH_GENERIC");  // read per launch: tests switch it inside one process
     return e != nullptr && e[0] != '0';
@@ -2607,7 +2607,9 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     // grid-stride cap: each block stages the leaf records once, so fewer,
     // longer-lived blocks (2048 was best of 1024..8192 with 96M-path pools;
     // 1024 with the 288M-path pools: +1.5 % C2, 512 -14 %: profiles/r02/shadeb/)
-    constexpr uint32_t max_blocks = 1024;            // (rt_api's shard slack assumes <= 4096, a multiple of 8)
+    // (rt_api's shard slack assumes <= 4096, a multiple of 8).  2048 / 4096 blocks for the sparse metal /
+    // dielectric queues measured the same as 1024 (profiles/r03/ab/ab_sparse_grid.log)
+    constexpr uint32_t max_blocks = 1024;
     uint32_t blocks = (n_upper + 255u) / 256u;
     blocks = (blocks + kShards - 1) / kShards * kShards;     // every shard gets the same number of blocks
     if (blocks > max_blocks) blocks = max_blocks;

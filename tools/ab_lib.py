@@ -2,7 +2,8 @@
 """A/B timing of two (or more) builds of librtamd.so on one GPU, with an image
 checksum per variant (the variants must render the same image bit for bit).
 
-usage: python tools/ab_lib.py --scene curves --spp 4 --rounds 2 base:path/to/librtamd_base.so new:path/to/librtamd.so
+usage: python tools/ab_lib.py --scene curves --spp 4 --rounds 2 base:path/to/librtamd_base.so new:path/to/librtamd.so \
+           leaf1:path/to/librtamd.so:RTAMD_BVH_LEAF=1
 Each (variant, round) is a separate process (RTAMD_LIB selects the library),
 rounds interleaved so box drift hits the variants alike.  Prints a line per
 run and a JSON summary (median Mrays/s, per-kernel ms of the last run)."""
@@ -27,7 +28,7 @@ def child(a):
     h = gpu.upload(sc)
     call("rt_set_profiling", h, 1)
     acc = torch.zeros(a.nx * a.ny * 3, dtype=torch.float64, device="cuda")
-    gpu.render_device(sc, a.nx, a.ny, 0, max(1, a.spp // 4), a.seed, acc.data_ptr())   # warm-up
+    gpu.render_device(sc, a.nx, a.ny, 0, a.spp, a.seed, acc.data_ptr())   # warm-up (sizes the path pools)
     acc.zero_()
     torch.cuda.synchronize()
     t = time.perf_counter()
@@ -56,8 +57,10 @@ def main():
     res = {}
     for r in range(a.rounds):
         for spec in a.variants:
-            name, _, lib = spec.partition(":")
+            name, _, rest = spec.partition(":")
+            lib, _, envs = rest.partition(":")
             env = dict(os.environ, RTAMD_LIB=os.path.abspath(lib))
+            env.update(dict(kv.split("=", 1) for kv in envs.split(",") if kv))
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--scene", a.scene, "--nx",
                                   str(a.nx), "--ny", str(a.ny), "--spp", str(a.spp), "--seed", str(a.seed)],
                                  env=env, capture_output=True, text=True, timeout=900)
