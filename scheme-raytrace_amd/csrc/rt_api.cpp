@@ -1084,6 +1084,15 @@ int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = 
     const char* e = std::getenv("RTAMD_LANES");
     return e ? std::max(1, std::atoi(e)) : 2;
 }
+// Scenes whose world BVH holds curves run the persistent curve kernel, whose
+// grid fills the chip by itself: a second lane's kernels only queue behind it
+// and its narrow tails, so one lane is faster (C5 at 64 spp: 200.3 vs 164.1
+// Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RTAMD_LANES overrides.
+int lanes_for(const DevScene& d) {
+    if (std::getenv("RTAMD_LANES")) return lanes_wanted();
+    const bool curve_kernel = d.n_bez > 0 && d.bvh_has_bez && d.n_med == 0 && d.n_klein == 0;
+    return curve_kernel ? 1 : lanes_wanted();
+}
 
 uint32_t tail_threshold() {
     const char* e = std::getenv("RTAMD_TAIL_PATHS");
@@ -1163,14 +1172,14 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     {
-        constexpr int min_chunks = 2;
+        const int min_chunks = lanes_for(s->dev);   // one chunk per lane at least
         int n = (int)((spp_count + chunk - 1) / chunk);
         if (n < min_chunks) n = std::min(min_chunks, spp_count);
         if (n > 1 && (n & 1) && n < spp_count) ++n;
         chunk = (uint32_t)((spp_count + n - 1) / n);
     }
     const int nchunks = (int)((spp_count + chunk - 1) / chunk);
-    const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_wanted()), nchunks));
+    const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_for(s->dev)), nchunks));
     const size_t cap = (size_t)npix * chunk;
     s->stats.chunks = (uint32_t)nchunks;
     s->stats.lanes = (uint32_t)nlanes;
