@@ -166,11 +166,22 @@ struct DevScene {
 // scattered rays all have time 0 (Q4), so deeper state has no time.
 // Records, not one array per field: a lane reads its ray with three 16-B
 // loads, and a kernel holds 4 base pointers instead of 13 (scalar registers).
+#ifdef RT_F32_RECORDS
+// Measurement build only ("f32 records"): ray and throughput
+// records stored in f32, all arithmetic still f64 — the record traffic an f32
+// perf mode would save, at the cost of parity.  Never the product build.
+struct alignas(8) RayRec { float ox, oy, oz, dx, dy, dz; };                   // 24 B
+struct alignas(8) PathRec { float tr, tg, tb; uint32_t wid, rng, pad; };
+static_assert(sizeof(PathRec) == 24, "PathRec layout");
+#else
 struct alignas(16) RayRec { double ox, oy, oz, dx, dy, dz; };                 // 48 B
+#endif
 // depth >= 1: throughput, work id, draw counter (32 B).  The depth is not
 // stored: every path of a wavefront iteration has the iteration's depth.
+#ifndef RT_F32_RECORDS
 struct alignas(8) PathRec { double tr, tg, tb; uint32_t wid, rng; };
 static_assert(sizeof(PathRec) == 32, "PathRec layout");
+#endif
 struct PathState {
     RayRec* ray;          // origin, direction
     PathRec* path;        // depth >= 1: throughput, work id, draw counter

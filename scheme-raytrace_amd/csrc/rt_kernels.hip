@@ -115,6 +115,19 @@ __device__ __forceinline__ v3 operator*(v3 a, double k) { return mk(a.x * k, a.y
 __device__ __forceinline__ double dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ double length(v3 a) { return sqrt(dot(a, a)); }
 __device__ __forceinline__ v3 unit(v3 a) { const double k = 1.0 / length(a); return a * k; }
+#ifdef RT_F32_RECORDS
+__device__ __forceinline__ RayRec ray_rec(const v3 o, const v3 d) {
+    return RayRec{(float)o.x, (float)o.y, (float)o.z, (float)d.x, (float)d.y, (float)d.z};
+}
+__device__ __forceinline__ PathRec path_rec(const v3 T, const uint32_t wid, const uint32_t rng) {
+    return PathRec{(float)T.x, (float)T.y, (float)T.z, wid, rng, 0u};
+}
+#else
+__device__ __forceinline__ RayRec ray_rec(const v3 o, const v3 d) { return RayRec{o.x, o.y, o.z, d.x, d.y, d.z}; }
+__device__ __forceinline__ PathRec path_rec(const v3 T, const uint32_t wid, const uint32_t rng) {
+    return PathRec{T.x, T.y, T.z, wid, rng};
+}
+#endif
 __device__ __forceinline__ v3 cross(v3 a, v3 b) {
     return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
@@ -191,7 +204,7 @@ __global__ __launch_bounds__(256) void k_raygen(const DevScene sc, const RenderP
     double time;
     Rng g;
     camera_ray(sc, rp, w, o, d, time, g);
-    st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};      // depth-0 state (rt_device.h PathState)
+    st.ray[w] = ray_rec(o, d);                             // depth-0 state (rt_device.h PathState)
     st.tm[w] = time;
     st.rng0[w] = g.ctr;
 }
@@ -1345,8 +1358,8 @@ __device__ __forceinline__ void load_path(const PathState& st, uint32_t i, PathR
 }
 // a scattered path (depth >= 1: no time)
 __device__ __forceinline__ void store_path(const PathState& st, uint32_t k, const PathRegs& p) {
-    st.ray[k] = RayRec{p.o.x, p.o.y, p.o.z, p.d.x, p.d.y, p.d.z};
-    st.path[k] = PathRec{p.T.x, p.T.y, p.T.z, p.wid, p.rng};
+    st.ray[k] = ray_rec(p.o, p.d);
+    st.path[k] = path_rec(p.T, p.wid, p.rng);
 }
 // a finished sample's colour: one 24-B record per work id (rgb together, so a
 // scattered sample write touches one 32-B sector instead of three lines)
@@ -1922,7 +1935,7 @@ __global__ __launch_bounds__(kExtLdsBlock, RT_CAMERA_WAVES) void k_camera(const 
                 const v3 L = sky_radiance(sc, d);            // throughput 1: (* 1 x) = x
                 put_sample(rp, w, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
             } else {
-                st.ray[w] = RayRec{o.x, o.y, o.z, d.x, d.y, d.z};   // depth-0 state for the shade kernels
+                st.ray[w] = ray_rec(o, d);                          // depth-0 state for the shade kernels
                 st.tm[w] = time;
                 st.rng0[w] = g.ctr;
                 hr = HitRec{t, leaf, w};

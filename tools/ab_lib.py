@@ -36,7 +36,11 @@ def child(a):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     st = gpu.stats(h)
-    digest = hashlib.sha1(acc.cpu().numpy().tobytes()).hexdigest()[:16]
+    img = acc.cpu().numpy()
+    digest = hashlib.sha1(img.tobytes()).hexdigest()[:16]
+    if a.out:
+        import numpy as np
+        np.save(a.out, img)
     print(json.dumps({"mrays": st.segments / dt / 1e6, "ms": dt * 1e3, "segments": st.segments, "sha": digest,
                       "ms_extend": st.ms_extend, "ms_shade": st.ms_shade, "ms_finish": st.ms_finish}), flush=True)
 
@@ -50,6 +54,7 @@ def main():
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--child", action="store_true")
+    p.add_argument("--out", default=None, help="(child) save the accumulator here (.npy)")
     p.add_argument("variants", nargs="*")
     a = p.parse_args()
     if a.child:
@@ -61,8 +66,10 @@ def main():
             lib, _, envs = rest.partition(":")
             env = dict(os.environ, RTAMD_LIB=os.path.abspath(lib))
             env.update(dict(kv.split("=", 1) for kv in envs.split(",") if kv))
+            img_path = "/tmp/ab_lib_%s.npy" % name
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--scene", a.scene, "--nx",
-                                  str(a.nx), "--ny", str(a.ny), "--spp", str(a.spp), "--seed", str(a.seed)],
+                                  str(a.nx), "--ny", str(a.ny), "--spp", str(a.spp), "--seed", str(a.seed),
+                                  "--out", img_path],
                                  env=env, capture_output=True, text=True, timeout=900)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")]
             if out.returncode != 0 or not line:
@@ -74,6 +81,13 @@ def main():
                   % (r, name, d["mrays"], d["ms"], d["sha"], d["ms_extend"], d["ms_shade"], d["ms_finish"]), flush=True)
     summ = {n: {"median_mrays": statistics.median(x["mrays"] for x in v), "sha": sorted({x["sha"] for x in v})}
             for n, v in res.items()}
+    import numpy as np
+    names = [spec.partition(":")[0] for spec in a.variants]
+    ref = np.load("/tmp/ab_lib_%s.npy" % names[0]) / a.spp
+    for n in names[1:]:
+        d = np.abs(np.load("/tmp/ab_lib_%s.npy" % n) / a.spp - ref)
+        summ[n]["rms_vs_" + names[0]] = float(np.sqrt(np.mean(d ** 2)))
+        summ[n]["pixels_gt_1e-9"] = int((d.reshape(-1, 3).max(axis=1) > 1e-9).sum())
     print(json.dumps(summ))
 
 

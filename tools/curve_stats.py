@@ -39,6 +39,9 @@ def main():
         "steps_per_survivor": b[34] / max(1, b[38]), "rederived_per_survivor": b[35] / max(1, b[38]),
         "rederive_splits_per_survivor": b[36] / max(1, b[38]), "leaf_tests_per_survivor": b[37] / max(1, b[38]),
         "kernel_lane_busy": b[21] / max(1, 64 * b[23]),
+        "kernel_lane_bvh_step": b[20] / max(1, 64 * b[23]), "kernel_lane_wait": b[22] / max(1, 64 * b[23]),
+        "kernel_iters_per_wave": b[23] / waves, "flushes_per_wave": b[25] / waves,
+        "kernel_clock_per_iter": b[40] / max(1, b[23]),
     }
     print(json.dumps(out, indent=1))
 
