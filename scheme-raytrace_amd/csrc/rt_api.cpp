@@ -46,16 +46,6 @@ hipError_t set_reject_cap(int);
 using namespace rtamd;
 
 namespace {
-// share (percent, env; default all) of a persistent kernel's resident blocks
-// it is launched with: fewer leave room for the other lane's kernels (A/B)
-uint32_t grid_share(const uint32_t resident, const char* env) {
-    const char* e = std::getenv(env);
-    const unsigned long pct = e ? std::strtoul(e, nullptr, 10) : 100ul;
-    if (pct >= 100ul) return resident;
-    const uint32_t b = (uint32_t)((uint64_t)resident * (pct ? pct : 1ul) / 100ul) / 8u * 8u;
-    return b >= 8u ? b : 8u;
-}
-
 thread_local std::string g_err;
 int fail(const std::string& msg) { g_err = msg; return 1; }
 
@@ -639,7 +629,6 @@ int commit_scene(Scene* s, int world) {
         // SAH sweep below 65 536 primitives, +1.5 % / +0.6 % over two per leaf: profiles/r02/ab_c5,
         // profiles/r03/c5walk/ab_leaf1.log)
         bb.leaf_max = 1;
-        if (const char* e = std::getenv("RTAMD_BVH_LEAF")) bb.leaf_max = std::max(1, std::atoi(e));
         bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
                                      std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));
         bb.build(0, (int)refs.size(), 0);
@@ -1006,7 +995,7 @@ int commit_scene(Scene* s, int world) {
         uint32_t mb = 0;
         if (lds > 0 && lds <= extend_lds_budget() && extend_lds_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
             s->ext_lds = lds;
-            s->ext_lds_blocks = grid_share(mb, "RTAMD_EXT_PCT");
+            s->ext_lds_blocks = mb;           // every resident block (50-88 % of them: -0.3 .. -3 %, profiles/r02/pct)
         }
         (void)hipGetLastError();
     }
@@ -1017,7 +1006,7 @@ int commit_scene(Scene* s, int world) {
         uint32_t mb = 0;
         if (lds > 0 && lds <= extend_lds_budget() && camera_prepare(d, lds, &mb) == hipSuccess && mb >= 256) {
             s->cam_lds = lds;
-            s->cam_blocks = grid_share(mb, "RTAMD_CAM_PCT");
+            s->cam_blocks = mb;
         }
         (void)hipGetLastError();
     }

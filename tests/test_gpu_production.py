@@ -258,11 +258,12 @@ def test_pools_shared_per_context_and_released(gpu_ctx, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("switch", ["RTAMD_NO_EXTEND_LDS", "RTAMD_NO_CAMERA_LDS", "RTAMD_FINISH_GENERIC"])
+@pytest.mark.parametrize("switch", ["RTAMD_NO_EXTEND_LDS", "RTAMD_NO_CAMERA_LDS", "RTAMD_FINISH_GENERIC", "RTAMD_NO_SOLO"])
 def test_kernel_variants_bitwise(gpu_ctx, monkeypatch, switch):
     """The cover scene's specialised kernels (k_extend_lds, k_camera, the SOLO
-    tail) against the general ones (k_extend<F>, k_raygen + k_extend, the
-    group-loop tail): the same image bit for bit."""
+    tail, the SOLO direct-leaf walk) against the general ones (k_extend<F>,
+    k_raygen + k_extend, the group-loop tail, leaf records): the same image
+    bit for bit."""
     nx, ny, spp = 64, 36, 3
     if switch != "RTAMD_FINISH_GENERIC":
         _wavefront_only(monkeypatch)
