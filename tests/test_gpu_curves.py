@@ -100,7 +100,7 @@ def _flat_curve_scene(nx, ny):
 def test_flat_curves_in_pooled_batches_vs_oracle(gpu_ctx, oracle_mod, monkeypatch):
     """Flat curves reach the pooled stage B of k_extend_curves (counted on the
     device), the render raises no fault, and the image matches the oracle."""
-    nx, ny, spp = 128, 128, 16          # a flipped sample moves its pixel by ~1e-2 / spp
+    nx, ny, spp = 128, 128, 64          # a flipped sample moves its pixel by ~1e-2 / spp
     sc = _flat_curve_scene(nx, ny)
     _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=1)
     acc = np.zeros(nx * ny * 3)
