@@ -650,6 +650,15 @@ int commit_scene(Scene* s, int world) {
         flatten_bvh2(bvh_nodes, margin, [&](int b, int e) {
             return BvhLeaf{ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0};
         }, bvh2, bleaf, bvh2_root, lane_stack);
+        if (bvh_has_bez) {                               // single-curve leaves: direct refs (kDirectCurve)
+            auto direct = [&](int32_t& ref) {
+                if (ref >= 0) return;
+                const BvhLeaf& L = bleaf[~ref];
+                if (L.sn == 0 && L.mn == 0 && L.bn == 1 && L.bb < kDirectCurve) ref = ~(kDirectCurve + L.bb);
+            };
+            for (BvhNode2& M : bvh2) { direct(M.l); direct(M.r); }
+            direct(bvh2_root);
+        }
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
             const LeafTmp& L = f.leaves[r.leaf];

@@ -76,6 +76,10 @@ struct MediumRec { int32_t bg_begin, bg_end, pad0, pad1; double neg_inv_density,
 // packed f32 FMAs (v_pk_fma_f32) on adjacent register pairs.
 struct alignas(64) BvhNode2 { float b[12]; int32_t l, r, pad0, pad1; };
 struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / moving / curve ranges
+// Trees that hold curves: a leaf holding exactly one curve k (and nothing
+// else) is referenced as ~(kDirectCurve + k), so a walk queues the curve from
+// the child ref itself instead of fetching a BvhLeaf record.
+constexpr int32_t kDirectCurve = 1 << 30;
 constexpr int kLaneStack = 32;                 // max per-lane traversal stack (dynamic LDS, stride = block size)
 
 // Shade-side per-leaf record (indexed by leaf id): what a shade kernel reads

@@ -1010,6 +1010,17 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                     --sp;
                     node = (int32_t)lstk[sp * stride];
                 }
+            } else if (~node >= kDirectCurve) {               // a leaf holding one curve
+                pb = ~node - kDirectCurve; pe = pb + 1;
+#ifdef RT_STATS
+                ++n_leaf; ++n_cand;
+#endif
+                if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
             } else {
                 const BvhLeaf L = sc.bleaf[~node];
                 for (int s = L.sb; s < L.sb + L.sn; ++s) {
@@ -1679,6 +1690,24 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
                 } else if (hr) {
                     node = N.r;
                 } else if (sp == 0) {
+                    trav = false;
+                } else {
+                    --sp;
+                    node = (int32_t)lstk[sp * stride];
+                }
+                // a leaf holding one curve: queued from its ref in this step (no leaf record, no extra step)
+                if (trav && ~node >= kDirectCurve) {
+                    pb = ~node - kDirectCurve; pe = pb + 1;
+                    if (sp == 0) {
+                        trav = false;
+                    } else {
+                        --sp;
+                        node = (int32_t)lstk[sp * stride];
+                    }
+                }
+            } else if (~node >= kDirectCurve) {                   // the root, or a popped direct leaf
+                pb = ~node - kDirectCurve; pe = pb + 1;
+                if (sp == 0) {
                     trav = false;
                 } else {
                     --sp;
