@@ -184,3 +184,41 @@ def test_duplicate_curves_tie_to_the_later_curve(gpu_ctx, oracle_mod, monkeypatc
     rms, dmax, nbad, npx = _compare(acc, ref, 4)
     print("duplicate curves render: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
     assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
+
+
+def test_few_curves_among_spheres_large_launch(gpu_ctx, oracle_mod, monkeypatch):
+    """Two curves in the cover scene's world BVH (random-scene, main.scm:31-88,
+    with its spheres), 960x540x16 spp in one chunk: 8.3M paths, thousands
+    of rays per wave of the persistent curve kernel.  Candidates are rare, so a
+    lane that queued one waits many loop iterations for a batch while the
+    other lanes keep claiming rays; the per-ray iteration cap counts only the
+    lane's own work, so a valid render raises no fault (round-2 advice: the
+    cap once counted the waiting too and scaled with the launch, not the
+    scene).  The image equals the per-ray curve kernel's bit for bit, and a
+    band of it matches the oracle."""
+    from rtamd.rng import HostStream
+    nx, ny, spp = 960, 540, 16
+    objs = scenes.random_scene_objects(HostStream(scenes.SCENE_SEED))
+    gold = g.make_metal(g.constant_texture(v.vec3(0.8, 0.6, 0.2)), 0.05)
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    objs.append(g.make_bezier(v.vec3(-6, 0.3, -2), v.vec3(-2, 2.5, 1), v.vec3(2, -0.5, 2), v.vec3(6, 1.5, -1),
+                              0.15, gold))
+    objs.append(g.make_bezier(v.vec3(-3, 2.0, 3), v.vec3(0, 0.5, -3), v.vec3(3, 3.0, 1), v.vec3(5, 0.8, 2), 0.1, red))
+    sc = g.make_scene(objs, scenes.camera_for(nx, ny), g.sky_color)
+    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=1, RTAMD_MAX_PATHS=nx * ny * spp)
+    acc = np.zeros(nx * ny * 3)
+    h = gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
+    st = gpu.stats(h)
+    assert st.chunks == 1 and st.finish_paths == 0, (st.chunks, st.finish_paths)
+    monkeypatch.setenv("RTAMD_CURVE_BLOCKS", "0")                  # the per-ray curve kernel
+    b = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, spp, SEED, b)
+    assert np.isfinite(acc).all() and np.array_equal(acc, b), np.abs(acc - b).max()
+    y0, rows = 250, 8
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    ref = np.zeros(nx * ny * 3)
+    oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, ref, lo, hi, nthreads=host_threads())
+    rms, dmax, nbad, npx = _compare(acc[3 * lo:3 * hi], ref[3 * lo:3 * hi], spp)
+    print("few curves among spheres: segments %d, rows %d..%d vs oracle rms=%.3e max=%.3e pixels>1e-9: %d/%d"
+          % (st.segments, y0, y0 + rows - 1, rms, dmax, nbad, npx))
+    assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
