@@ -52,6 +52,15 @@ EXTEND_BYTES_PER_SEGMENT = 48 + 16
 EXTEND_BYTES_PER_PATH = 12 + (52 - 16)
 
 
+def extend_kernels(scene, info):
+    """The kernels whose launches the extend events bracket (roofline*.kernel)."""
+    if scene == "curves":
+        return "k_extend_curves (persistent, every depth)"
+    if info.get("camera_lds_bytes"):
+        return "k_camera (depth 0) + k_extend_lds"
+    return "k_extend_lds" if info.get("extend_lds_bytes") else "k_extend"
+
+
 def extend_bytes(segments, paths):
     return EXTEND_BYTES_PER_SEGMENT * segments + EXTEND_BYTES_PER_PATH * paths
 
@@ -355,6 +364,7 @@ def main():
         valu = None
         valu_issue = None
         roof_iso = None
+        ext_kernels = extend_kernels(a.scene, gpu.scene_info(h))
         pm = None                       # PMC bytes / issue counters of the extend kernels (tools/profile_round.sh)
         pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
         if os.path.exists(pmc):
@@ -367,7 +377,7 @@ def main():
             ams = iso.ms_extend / iso.extend_launches
             ach = bpl / (ams * 1e-3) / 1e9
             roof_iso = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": "k_extend + k_extend_lds",
+                        "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": ext_kernels,
                         "bytes_per_launch": round(bpl), "rays_per_launch": round(iso.extend_rays / iso.extend_launches),
                         "avg_launch_ms": round(ams, 4),
                         "traffic": round(pm["bytes_per_segment"] * iso.extend_rays / iso.extend_launches) if pm else None,
@@ -384,7 +394,7 @@ def main():
                 traffic = round(pm["bytes_per_segment"] * rays_per_launch)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": "k_extend + k_extend_lds", "bytes_per_launch": round(bytes_per_launch),
+                    "kernel": ext_kernels, "bytes_per_launch": round(bytes_per_launch),
                     "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4),
                     "note": "timed region; render lanes overlap, so launch durations include concurrent kernels"}
             if pm and pm.get("valu_busy") is not None:

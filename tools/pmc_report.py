@@ -121,7 +121,7 @@ def main():
         report["kernels"][f] = r
 
     # the extend phase (k_camera at depth 0, k_extend_lds / k_extend deeper): bench.py's roofline.traffic
-    ext = [f for f in ("k_camera", "k_extend_lds", "k_extend") if f in fams]
+    ext = [f for f in ("k_camera", "k_extend_lds", "k_extend", "k_extend_curves") if f in fams]
     fb = sum(tot(f, "FETCH_SIZE") for f in ext) * 1024
     wb = sum(tot(f, "WRITE_SIZE") for f in ext) * 1024
     f64 = sum((tot(f, "SQ_INSTS_VALU_ADD_F64") + tot(f, "SQ_INSTS_VALU_MUL_F64") + 2 * tot(f, "SQ_INSTS_VALU_FMA_F64")
