@@ -147,6 +147,7 @@ struct Scene {
     DevScene dev{};
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
+    DevBuf d_bvh4, d_stk_ovf;                      // curve trees: BVH4 and the walk's stack overflow
     DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
     DevBuf d_leaf_cls;
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
@@ -521,6 +522,69 @@ void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_
     for (int dd : depth) lane_stack = std::max(lane_stack, dd);
 }
 
+// The BVH4 of a BVH2 (BvhNode4): node p's children, an inner child replaced
+// by its own two children with their boxes as the BVH2 stores them.  Returns
+// the root ref; stack4 = the most stack entries its walk can hold (a node
+// pushes all but the child it enters: the sum of (children - 1) along a path).
+int32_t collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, std::vector<BvhNode4>& bvh4, int32_t& stack4) {
+    stack4 = 0;
+    if (root < 0) return root;
+    struct Slot { int32_t ref; float lo[3], hi[3]; };
+    auto child = [&](const BvhNode2& M, const int side, Slot& o) {          // side 0 = l, 1 = r
+        o.ref = side ? M.r : M.l;
+        for (int k = 0; k < 3; ++k) { o.lo[k] = M.b[2 * k + side]; o.hi[k] = M.b[6 + 2 * k + side]; }
+    };
+    // iterative: (bvh2 node, bvh4 index) pairs still to fill
+    std::vector<std::pair<int32_t, int32_t>> todo{{root, 0}};
+    std::vector<int32_t> need;                     // per bvh4 node: children - 1
+    std::vector<std::vector<int32_t>> kids;        // per bvh4 node: inner bvh4 children
+    bvh4.assign(1, BvhNode4{});
+    need.assign(1, 0);
+    kids.assign(1, {});
+    while (!todo.empty()) {
+        const auto [p, q] = todo.back();
+        todo.pop_back();
+        Slot sl[4];
+        int n = 0;
+        for (int side = 0; side < 2; ++side) {
+            Slot c;
+            child(bvh2[p], side, c);
+            if (c.ref >= 0) { child(bvh2[c.ref], 0, sl[n++]); child(bvh2[c.ref], 1, sl[n++]); }
+            else sl[n++] = c;
+        }
+        BvhNode4 N{};
+        for (int j = 0; j < 4; ++j)
+            for (int k = 0; k < 3; ++k) { N.lo[k][j] = 0.0f; N.hi[k][j] = -1.0f; }   // empty: never read (j >= n)
+        N.n = n;
+        for (int j = 0; j < n; ++j) {
+            for (int k = 0; k < 3; ++k) { N.lo[k][j] = sl[j].lo[k]; N.hi[k][j] = sl[j].hi[k]; }
+            if (sl[j].ref >= 0) {
+                const int32_t q2 = (int32_t)bvh4.size();
+                bvh4.push_back(BvhNode4{});
+                need.push_back(0);
+                kids.push_back({});
+                kids[q].push_back(q2);
+                todo.push_back({sl[j].ref, q2});
+                N.ref[j] = q2;
+            } else {
+                N.ref[j] = sl[j].ref;
+            }
+        }
+        for (int j = n; j < 4; ++j) N.ref[j] = sl[0].ref;
+        bvh4[q] = N;
+        need[q] = n - 1;
+    }
+    // children were appended after their parents: fold the stack bound bottom-up
+    std::vector<int32_t> deep(bvh4.size(), 0);
+    for (size_t q = bvh4.size(); q-- > 0;) {
+        int32_t m = 0;
+        for (int32_t c : kids[q]) m = std::max(m, deep[c]);
+        deep[q] = need[q] + m;
+    }
+    stack4 = deep[0];
+    return 0;
+}
+
 size_t extend_lds_budget() { return (size_t)64 << 10; }   // largest LDS footprint k_extend_lds may take
 
 int commit_scene(Scene* s, int world) {
@@ -613,6 +677,8 @@ int commit_scene(Scene* s, int world) {
     std::vector<BvhLeaf> bleaf;
     int32_t bvh2_root = 0;
     int32_t lane_stack = 0;
+    std::vector<BvhNode4> bvh4;                      // curve trees (k_extend_curves)
+    int32_t bvh4_root = 0, stack4 = 0;
     bool bvh_has_bez = false;
     float bvh_pad = 0.0f;
     double margin = 0.0;
@@ -658,6 +724,7 @@ int commit_scene(Scene* s, int world) {
             };
             for (BvhNode2& M : bvh2) { direct(M.l); direct(M.r); }
             direct(bvh2_root);
+            bvh4_root = collapse_bvh4(bvh2, bvh2_root, bvh4, stack4);
         }
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
@@ -942,6 +1009,20 @@ int commit_scene(Scene* s, int world) {
     d.n_bleaf = (int)bleaf.size();
     d.lane_stack = lane_stack;
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
+    if (!bvh4.empty()) {
+        if (int rc = upload(s->d_bvh4, bvh4, &d.bvh4)) return rc;
+        d.n_bvh4 = (int)bvh4.size();
+        d.bvh4_root = bvh4_root;
+        d.stack4 = stack4;
+        if (stack4 > lane_stack) {                   // the walk's deepest stacks spill past the LDS columns
+            int dev = 0, cus = 0;
+            HIPCHK(hipGetDevice(&dev));
+            HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            d.ovf_lanes = (uint32_t)std::max(cus, 1) * 2048u;     // any resident grid of 256-thread blocks
+            HIPCHK(s->d_stk_ovf.ensure((size_t)d.ovf_lanes * (size_t)(stack4 - lane_stack) * sizeof(uint32_t)));
+            d.stk_ovf = s->d_stk_ovf.as<uint32_t>();
+        }
+    }
     if (int rc = upload(s->d_chains, chains, &d.chains)) return rc;
     if (int rc = upload(s->d_leaves, leaves, &d.leaves)) return rc;
     {

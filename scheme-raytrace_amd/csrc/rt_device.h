@@ -80,6 +80,14 @@ struct BvhLeaf { int32_t sb, sn, mb, mn, bb, bn, pad0, pad1; };   // sphere / mo
 // else) is referenced as ~(kDirectCurve + k), so a walk queues the curve from
 // the child ref itself instead of fetching a BvhLeaf record.
 constexpr int32_t kDirectCurve = 1 << 30;
+// The curve tree as a BVH4 for the persistent curve kernel (k_extend_curves):
+// each BVH2 inner node with an inner child replaced by that child's two
+// children (the BVH2's own f32 boxes, so culling stays as conservative), so a
+// walk through a tree far larger than the L2 pays one dependent 128-B fetch
+// per two levels.  Planes as [axis][child]; child refs as in BvhNode2 (>= 0
+// an inner BvhNode4, < 0 a leaf / direct curve); children [n, 4) are empty.
+struct alignas(128) BvhNode4 { float lo[3][4]; float hi[3][4]; int32_t ref[4]; int32_t n, pad0, pad1, pad2; };
+static_assert(sizeof(BvhNode4) == 128, "BvhNode4 is one 128-B line");
 constexpr int kLaneStack = 32;                 // max per-lane traversal stack (dynamic LDS, stride = block size)
 
 // Shade-side per-leaf record (indexed by leaf id): what a shade kernel reads
@@ -132,6 +140,12 @@ struct DevScene {
     int32_t bvh_has_bez;                           // curves in the BVH: widen the box t range (see bvh_closest)
     float bvh_pad;                                 // the margin baked into the f32 boxes (diagnostic)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
+    // BVH4 of the same tree (curve trees only, else nullptr): its walk pushes up to three children per
+    // node, stack4 entries at most; entries past the LDS stack (lane_stack) go to stk_ovf, stack4 -
+    // lane_stack words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g)
+    const BvhNode4* bvh4;  int32_t n_bvh4;
+    int32_t bvh4_root, stack4;
+    uint32_t* stk_ovf;     uint32_t ovf_lanes;
     // Time-0 tree over the same primitives (nullptr = none): every moving
     // sphere frozen at center(0), so rays with time +0.0 (all scattered rays,
     // Q4) traverse tighter boxes.  Leaves index fsph (plain sphere records in

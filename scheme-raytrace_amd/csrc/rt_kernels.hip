@@ -346,13 +346,21 @@ __device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay
 // right half in registers instead cut the re-derivation splits per curve from
 // 15 to 5 at C5, but the persistent curve kernel then spills: 120.6 vs 137.8
 // Mrays/s at 4 spp.)
+//
+// Uniform work per call (round 3): a call does ONE split — a descent split
+// (both halves culled) or one level of a right sibling's re-derivation from
+// the root — or, separately, one leaf test (bez_walk_leaf), so the lanes of a
+// wave run the same code in the same iteration.  (One call per node, with
+// the whole re-derivation loop and the leaf test inside, made every wave
+// iteration cost the longest re-derivation among its lanes plus a leaf test.)
 struct BezWalk {
     Bez4 root, c;
     double best, tmax, w1, w2;
     int L, leaf_level, base;        // base: the level the walk started at (a donated subtree's root; else 0)
+    int rl;                         // re-derivation (!fresh): c is the path node at level rl < L
     uint32_t idx, it, cap;
     uint32_t rmask;                 // bit L: the right sibling of the level-L left half was culled at the split
-    bool fresh, found;              // fresh: c is valid and passed the cull
+    bool fresh, found;              // fresh: c is node (L, idx) and passed the cull
 };
 // converge's subdivision depth from the transformed curve's flatness (:180-193)
 __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
@@ -373,10 +381,14 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
     s.root = root; s.c = root;
     s.w1 = w1; s.w2 = w2; s.tmax = tmax;
     s.leaf_level = leaf_level;
-    s.cap = 4u << s.leaf_level;              // each of the <= 2^(leaf_level+1) nodes is visited at most once
-    s.L = 0; s.base = 0; s.idx = 0; s.it = 0; s.rmask = 0;
+    // each of the <= 2^(leaf_level+1) nodes is visited at most once, for at
+    // most leaf_level re-derivation splits and one split or leaf test
+    s.cap = (uint32_t)(s.leaf_level + 2) << (s.leaf_level + 1);
+    s.L = 0; s.base = 0; s.rl = 0; s.idx = 0; s.it = 0; s.rmask = 0;
     s.fresh = true; s.found = false; s.best = tmax;
 }
+// at a leaf segment: the next call is bez_walk_leaf
+__device__ __forceinline__ bool bez_walk_at_leaf(const BezWalk& s) { return s.fresh && s.L >= s.leaf_level; }
 // set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
 // stage A's root cull) is given; false if the whole curve is culled
 __device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
@@ -387,67 +399,90 @@ __device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, c
     bez_walk_init(s, root, B.w1, B.w2, tmax, leaf_level);
     return true;
 }
-// one node of the walk; true once the walk is over
-__device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
+// past the current node: climb past right halves and past left halves whose
+// right sibling was culled at the split, then aim at the surviving right
+// sibling (re-derived from the root); true once the walk is over
+__device__ __forceinline__ bool bez_walk_next(BezWalk& s) {
+    while (s.L > s.base && ((s.idx & 1u) || ((s.rmask >> s.L) & 1u))) { --s.L; s.idx >>= 1; }
+    if (s.L == s.base) return true;
+    ++s.idx;
+    s.c = s.root; s.rl = 0; s.fresh = false;
+    return false;
+}
+// one split (not at a leaf: !bez_walk_at_leaf); true once the walk is over
+__device__ __forceinline__ bool bez_walk_split(BezWalk& s) {
     if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
-    bool live = true;
-    if (!s.fresh) {                                             // a right sibling that survived its split
+    Bez4 l, r;
+    bez_split(s.c, l, r);                                       // split, left first (:167-175)
+    // (:123-128) with the best z so far
+    const bool kl = !bez_culled(l, s.w1, s.best), kr = !bez_culled(r, s.w1, s.best);
+    if (!s.fresh) {                                             // one level toward the right sibling (L, idx)
+        const bool right = (s.idx >> (s.L - 1 - s.rl)) & 1u;
+        s.c = right ? r : l;
+        if (++s.rl < s.L) return false;
+        if (right ? kr : kl) { s.fresh = true; return false; }  // it survives the cull: visit it
+        return bez_walk_next(s);
+    }
+    if (kl || kr) {
+        ++s.L;
+        if (kl) {
+            s.c = l; s.idx <<= 1;
+            s.rmask = kr ? (s.rmask & ~(1u << s.L)) : (s.rmask | (1u << s.L));
+        } else {
+            s.c = r; s.idx = (s.idx << 1) | 1u;
+        }
+        return false;
+    }
+    return bez_walk_next(s);
+}
+// one node (not at a leaf): a pending right sibling is re-derived from the
+// root in one go, then split; true once the walk is over
+__device__ __forceinline__ bool bez_walk_node(BezWalk& s) {
+    if (!s.fresh) {
+        if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
         s.c = s.root;
         for (int k = s.L - 1; k >= 0; --k) {
             Bez4 l, r;
             bez_split(s.c, l, r);
             s.c = ((s.idx >> k) & 1u) ? r : l;
         }
-        live = !bez_culled(s.c, s.w1, s.best);                  // (:123-128) with the best z so far
+        if (bez_culled(s.c, s.w1, s.best)) return bez_walk_next(s);
+        s.rl = s.L;
+        s.fresh = true;
+        if (s.L >= s.leaf_level) return false;                  // a leaf: tested in a leaf phase
     }
-    s.fresh = false;
-    if (live) {
-        const Bez4& c = s.c;
-        if (s.L < s.leaf_level) {                               // split, left first (:167-175)
-            Bez4 l, r;
-            bez_split(c, l, r);
-            const bool kl = !bez_culled(l, s.w1, s.best), kr = !bez_culled(r, s.w1, s.best);
-            if (kl || kr) {
-                ++s.L;
-                if (kl) {
-                    s.c = l; s.idx <<= 1;
-                    s.rmask = kr ? (s.rmask & ~(1u << s.L)) : (s.rmask | (1u << s.L));
-                } else {
-                    s.c = r; s.idx = (s.idx << 1) | 1u;
-                }
-                s.fresh = true;
-                return false;
-            }
-        } else {
-            // leaf segment (:130-166)
-            const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
-            const v3 dir = c.p3 - c.p0;
-            v3 dp0 = bez_tan(c, false);
-            if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
-            if (!(dot2d(dp0, c.p0 * -1.0) < 0.0)) {
-                v3 dpn = bez_tan(c, true);
-                if (dot2d(dir, dpn) < 0.0) dpn = dpn * -1.0;
-                if (!(dot2d(dpn, c.p3) < 0.0)) {
-                    double w = dir.x * dir.x + dir.y * dir.y;
-                    if (w != 0.0) {
-                        w = (c.p0.x * dir.x + c.p0.y * dir.y) / (-w);
-                        w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
-                        const double v = v0 * (1.0 - w) + vn * w;
-                        const v3 p = bez_point(c, v);             // sub-curve at the global v (Q11)
-                        if (!(p.x * p.x + p.y * p.y >= s.w2 || p.z <= 0.0001 || s.tmax < p.z)) {
-                            if (!s.found || p.z < s.best) s.best = p.z;
-                            s.found = true;
-                        }
-                    }
+    return bez_walk_split(s);
+}
+// the leaf segment's test (:130-166) (bez_walk_at_leaf); true once the walk is over
+__device__ __forceinline__ bool bez_walk_leaf(BezWalk& s) {
+    if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
+    const Bez4& c = s.c;
+    const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
+    const v3 dir = c.p3 - c.p0;
+    v3 dp0 = bez_tan(c, false);
+    if (dot2d(dir, dp0) < 0.0) dp0 = dp0 * -1.0;
+    if (!(dot2d(dp0, c.p0 * -1.0) < 0.0)) {
+        v3 dpn = bez_tan(c, true);
+        if (dot2d(dir, dpn) < 0.0) dpn = dpn * -1.0;
+        if (!(dot2d(dpn, c.p3) < 0.0)) {
+            double w = dir.x * dir.x + dir.y * dir.y;
+            if (w != 0.0) {
+                w = (c.p0.x * dir.x + c.p0.y * dir.y) / (-w);
+                w = (w < 0.0) ? 0.0 : ((w > 1.0) ? 1.0 : w);
+                const double v = v0 * (1.0 - w) + vn * w;
+                const v3 p = bez_point(c, v);                   // sub-curve at the global v (Q11)
+                if (!(p.x * p.x + p.y * p.y >= s.w2 || p.z <= 0.0001 || s.tmax < p.z)) {
+                    if (!s.found || p.z < s.best) s.best = p.z;
+                    s.found = true;
                 }
             }
         }
     }
-    // climb past right halves and past left halves whose right sibling was culled at the split
-    while (s.L > s.base && ((s.idx & 1u) || ((s.rmask >> s.L) & 1u))) { --s.L; s.idx >>= 1; }
-    if (s.L == s.base) return true;
-    ++s.idx;                                                    // the surviving right sibling
-    return false;
+    return bez_walk_next(s);
+}
+// one call of the walk (a leaf test or a split); true once the walk is over
+__device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
+    return bez_walk_at_leaf(s) ? bez_walk_leaf(s) : bez_walk_split(s);
 }
 
 // Work sharing: the right siblings still pending on a walk's path (levels
@@ -524,6 +559,12 @@ constexpr int kBezRefill = 8;         // stage B: idle lanes that take the next 
 constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
 #ifndef RT_BEZ_HOLD
 #define RT_BEZ_HOLD 192                // stage B runs once this many root-cull survivors wait (multiple of 64)
+#endif
+#ifndef RT_BEZ_LEAF_PHASE
+#define RT_BEZ_LEAF_PHASE 32           // stage B: lanes at a leaf segment that test together
+#endif
+#ifndef RT_BEZ_WALK
+#define RT_BEZ_WALK 1                  // stage B node step: 1 = re-derivation in one go, 0 = one split per iteration
 #endif
 constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
 struct BezWave {
@@ -623,7 +664,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         uint32_t n_it = 0, n_busy = 0, n_step = 0, n_red = 0, n_rsplit = 0, n_leaf = 0;
         const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
 #endif
-        const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * ((4ull << (kBezMaxDepth + 1)) + 2ull);
+        const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * (((unsigned long long)(kBezMaxDepth + 3) << (kBezMaxDepth + 2)) + 2ull);
         for (unsigned long long g = 0;; ++g) {                    // wave-uniform
             if (g > guard_cap) { raise_fault(RT_FAULT_CURVE); break; }
 #ifdef RT_STATS
@@ -631,8 +672,8 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             n_busy += busy ? 1u : 0u;
             if (busy) {
                 ++n_step;
-                if (!wk.fresh) { ++n_red; n_rsplit += (uint32_t)wk.L; }
-                if (wk.L >= wk.leaf_level) ++n_leaf;
+                if (!wk.fresh) { n_red += wk.rl == 0 ? 1u : 0u; n_rsplit += RT_BEZ_WALK == 1 ? (uint32_t)wk.L : 1u; }
+                if (bez_walk_at_leaf(wk)) ++n_leaf;     // lane-iterations at a leaf (tested or waiting)
             }
 #endif
             const unsigned long long idle = __ballot(!busy);
@@ -671,11 +712,25 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     wave_sync();
                 }
             }
-            if (__ballot(busy) == 0ull) {
+            const unsigned long long bm = __ballot(busy);
+            if (bm == 0ull) {
                 if (cursor >= nb) break;
                 continue;
             }
-            if (busy && bez_walk_step(wk)) {
+            // lanes at a leaf segment wait until enough of them (or every busy lane) are there and
+            // then test together; the others split this iteration either way
+            const bool at_leaf = busy && bez_walk_at_leaf(wk);
+            const unsigned long long lm = __ballot(at_leaf);
+            bool over = false;
+            if (lm != 0ull && (__popcll(lm) >= RT_BEZ_LEAF_PHASE || lm == bm)) {
+                if (at_leaf) over = bez_walk_leaf(wk);
+            }
+#if RT_BEZ_WALK == 1
+            if (busy && !at_leaf) over = bez_walk_node(wk);
+#else
+            if (busy && !at_leaf) over = bez_walk_split(wk);
+#endif
+            if (over) {
                 if (wk.found)
                     atomicMin((unsigned long long*)&W.sz[si], (unsigned long long)__double_as_longlong(wk.best));
                 busy = false;
@@ -1592,8 +1647,21 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     double tm = 0.0, a = 0.0, ia = 0.0, tscale = 1.0, closest = kTmax;
     int32_t best = -1, node = 0;
     BoxRay br{};
-    BvhNode2 N{};                                   // the lane's next node, loaded one iteration ahead
+    BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
     int sp = 0, pb = 0, pe = 0;
+    // the walk's stack: LDS column for the first lmax entries, the global overflow area past them
+    const uint32_t ovf_lane = blockIdx.x * 256u + threadIdx.x;
+    const int scap = max(lmax, sc.stack4);          // commit_scene's bound on the walk's stack
+    auto push = [&](const int32_t e) {
+        if (sp >= scap) { raise_fault(RT_FAULT_PATH); return; }
+        if (sp < lmax) lstk[sp * stride] = (uint32_t)e;
+        else sc.stk_ovf[(size_t)(sp - lmax) * sc.ovf_lanes + ovf_lane] = (uint32_t)e;
+        ++sp;
+    };
+    auto pop = [&]() -> int32_t {
+        --sp;
+        return (int32_t)(sp < lmax ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lmax) * sc.ovf_lanes + ovf_lane]);
+    };
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
     // a ray takes at most one step per node / leaf and one queue step per two curves: bound its
     // working iterations (a valid walk stays far below)
@@ -1666,53 +1734,58 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
                     bez_ray(o, d, W.ray[lane]);
                     W.done[lane] = 0u;
                     queued = 0u;
-                    sp = 0; node = sc.bvh2_root; trav = gb < sc.n_groups; pb = pe = 0;
-                    if (trav && node >= 0) N = sc.bvh2[node];
+                    sp = 0; node = sc.bvh4_root; trav = gb < sc.n_groups; pb = pe = 0;
+                    if (trav && node >= 0) N = sc.bvh4[node];
                     active = true;
                     ray_it = 0;
                 }
             }
         }
         if (__ballot(active) == 0ull) break;         // every queued candidate has been resolved
-        // 3. one BVH step (bvh_closest_curves)
+        // 3. one BVH4 step (bvh_closest_curves over the collapsed tree): the node's hit children
+        //    nearest first, the nearest entered, the others pushed
         if (active && trav && pb >= pe) {
             if (node >= 0) {
                 const float tcap = f32_up(closest * tscale);
-                float tl, tr;
-                bool hl, hr;
-                node_hit(N, br, tcap, hl, hr, tl, tr);
-                if (hl && hr) {
-                    const bool lfirst = tl <= tr;
-                    if (sp < lmax) { lstk[sp * stride] = (uint32_t)(lfirst ? N.r : N.l); ++sp; }
-                    node = lfirst ? N.l : N.r;
-                } else if (hl) {
-                    node = N.l;
-                } else if (hr) {
-                    node = N.r;
-                } else if (sp == 0) {
-                    trav = false;
+                float key[4];
+                int32_t ref[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float tx0 = fmaf(N.lo[0][j], br.ix, -br.px), tx1 = fmaf(N.hi[0][j], br.ix, -br.px);
+                    const float ty0 = fmaf(N.lo[1][j], br.iy, -br.py), ty1 = fmaf(N.hi[1][j], br.iy, -br.py);
+                    const float tz0 = fmaf(N.lo[2][j], br.iz, -br.pz), tz1 = fmaf(N.hi[2][j], br.iz, -br.pz);
+                    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
+                    key[j] = (tn <= tf && j < N.n) ? tn : INFINITY;   // slab ends are finite: INFINITY = missed
+                    ref[j] = N.ref[j];
+                }
+                auto cswap = [&](const int x, const int y) {
+                    const bool sw = key[y] < key[x];
+                    const float kx = key[x];
+                    const int32_t rx = ref[x];
+                    key[x] = sw ? key[y] : kx; key[y] = sw ? kx : key[y];
+                    ref[x] = sw ? ref[y] : rx; ref[y] = sw ? rx : ref[y];
+                };
+                cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
+                if (key[0] == INFINITY) {
+                    if (sp == 0) trav = false;
+                    else node = pop();
                 } else {
-                    --sp;
-                    node = (int32_t)lstk[sp * stride];
+                    if (key[3] != INFINITY) push(ref[3]);
+                    if (key[2] != INFINITY) push(ref[2]);
+                    if (key[1] != INFINITY) push(ref[1]);
+                    node = ref[0];
                 }
                 // a leaf holding one curve: queued from its ref in this step (no leaf record, no extra step)
                 if (trav && ~node >= kDirectCurve) {
                     pb = ~node - kDirectCurve; pe = pb + 1;
-                    if (sp == 0) {
-                        trav = false;
-                    } else {
-                        --sp;
-                        node = (int32_t)lstk[sp * stride];
-                    }
+                    if (sp == 0) trav = false;
+                    else node = pop();
                 }
             } else if (~node >= kDirectCurve) {                   // the root, or a popped direct leaf
                 pb = ~node - kDirectCurve; pe = pb + 1;
-                if (sp == 0) {
-                    trav = false;
-                } else {
-                    --sp;
-                    node = (int32_t)lstk[sp * stride];
-                }
+                if (sp == 0) trav = false;
+                else node = pop();
             } else {
                 const BvhLeaf L = sc.bleaf[~node];
                 for (int s = L.sb; s < L.sb + L.sn; ++s) {
@@ -1726,16 +1799,12 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
                     sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
                 }
                 pb = L.bb; pe = L.bb + L.bn;
-                if (sp == 0) {
-                    trav = false;
-                } else {
-                    --sp;
-                    node = (int32_t)lstk[sp * stride];
-                }
+                if (sp == 0) trav = false;
+                else node = pop();
             }
         }
         // the next node's record, in flight while the batches below run (+5 % at C5)
-        if (active && trav && node >= 0) N = sc.bvh2[node];
+        if (active && trav && node >= 0) N = sc.bvh4[node];
         // 4. queue this step's curve candidates (at most 2 per lane)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
