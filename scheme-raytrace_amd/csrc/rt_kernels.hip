@@ -563,6 +563,9 @@ constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per
 #ifndef RT_BEZ_LEAF_PHASE
 #define RT_BEZ_LEAF_PHASE 32           // stage B: lanes at a leaf segment that test together
 #endif
+#ifndef RT_CURVE_FINISH_BATCH
+#define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
+#endif
 #ifndef RT_BEZ_WALK
 #define RT_BEZ_WALK 1                  // stage B node step: 1 = re-derivation in one go, 0 = one split per iteration
 #endif
@@ -1670,7 +1673,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
 #ifdef RT_STATS
     uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
     const unsigned long long st_clk0 = __builtin_amdgcn_s_memtime();
-    unsigned long long st_clk_a = 0;
+    unsigned long long st_clk_a = 0, st_clk1 = 0, st_clk2 = 0, st_clk3 = 0, st_t = 0;
 #endif
     for (;;) {
         // only iterations in which the lane itself works count: one waiting for a batch
@@ -1684,11 +1687,22 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         if (active) ++st_busy;
         if (active && !trav && pb >= pe) ++st_wait;
 #endif
+#ifdef RT_STATS
+        st_t = __builtin_amdgcn_s_memtime();
+#endif
         // 1. rays whose traversal ended and whose curves are all resolved: the
         //    groups after the BVH, then miss (sky) or hit + material queue
         int cls = -1;
         HitRec hr{};
-        if (active && !trav && pb >= pe && W.done[lane] == queued) {
+        // Finished lanes are written out (and refilled in step 2) together, once RT_CURVE_FINISH_BATCH of
+        // them are ready, every active lane is, or the ray list is exhausted: a miss's path-record gather,
+        // the queue append's returning atomics and the refill's claim and ray loads are dependent
+        // round trips, which cost the wave the same whether one lane or sixteen take them.
+        const bool fin = active && !trav && pb >= pe && W.done[lane] == queued;
+        const unsigned long long fin_m = __ballot(fin);
+        const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= RT_CURVE_FINISH_BATCH ||
+                                             fin_m == __ballot(active));
+        if (fin && flush) {
             for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
             if (best < 0) {
                 const v3 L = sky_radiance(sc, d);
@@ -1706,6 +1720,9 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         }
         const uint32_t slot = wave_append(cls, (k >> 8) & (uint32_t)(kShards - 1), counts, shard_cap);
         if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
+#ifdef RT_STATS
+        { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
+#endif
         // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
         const unsigned long long need = __ballot(!active);
         if (need && !exhausted) {
@@ -1742,6 +1759,9 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
             }
         }
         if (__ballot(active) == 0ull) break;         // every queued candidate has been resolved
+#ifdef RT_STATS
+        { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk2 += t - st_t; st_t = t; }
+#endif
         // 3. one BVH4 step (bvh_closest_curves over the collapsed tree): the node's hit children
         //    nearest first, the nearest entered, the others pushed
         if (active && trav && pb >= pe) {
@@ -1805,6 +1825,9 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         }
         // the next node's record, in flight while the batches below run (+5 % at C5)
         if (active && trav && node >= 0) N = sc.bvh4[node];
+#ifdef RT_STATS
+        { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk3 += t - st_t; st_t = t; }
+#endif
         // 4. queue this step's curve candidates (at most 2 per lane)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1846,7 +1869,8 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     RT_STAT(20, st_steps); RT_STAT(21, st_busy); RT_STAT(22, st_wait);
     if (lane == 0u) {
         RT_STAT(23, st_iter); RT_STAT(24, 1); RT_STAT(25, st_flush);
-        RT_STAT(40, __builtin_amdgcn_s_memtime() - st_clk0); RT_STAT(41, st_clk_a);   // kernel / stage A clocks per wave
+        RT_STAT(40, __builtin_amdgcn_s_memtime() - st_clk0); RT_STAT(41, st_clk_a);
+        RT_STAT(42, st_clk1); RT_STAT(43, st_clk2); RT_STAT(44, st_clk3);   // kernel / stage A clocks per wave
     }
 #endif
 }
