@@ -231,7 +231,7 @@ typedef struct rt_scene_info {
     uint32_t extend_lds_bytes, extend_lds_blocks;   /* k_extend_lds: LDS per block, resident blocks */
     uint32_t camera_lds_bytes, camera_lds_blocks;   /* k_camera: the same */
     int32_t  cus;             /* compute units of the context's device */
-    int32_t  reserved;
+    int32_t  curve_stack;     /* curve trees: stack entries the BVH4 walk of k_extend_curves may hold (0: none) */
 } rt_scene_info;
 int rt_get_scene_info(int scene, rt_scene_info* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */

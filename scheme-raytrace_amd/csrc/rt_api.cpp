@@ -1874,6 +1874,7 @@ int rt_get_scene_info(int scene, rt_scene_info* out) {
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     out->cus = cus;
+    out->curve_stack = d.bvh4 ? d.stack4 : 0;
     return 0;
 }
 

@@ -361,6 +361,8 @@ struct BezWalk {
     uint32_t idx, it, cap;
     uint32_t rmask;                 // bit L: the right sibling of the level-L left half was culled at the split
     bool fresh, found;              // fresh: c is node (L, idx) and passed the cull
+    uint8_t stg;                    // staged (bez_walk_stage): c holds the curve's raw control points; 1 = a
+                                    // survivor's walk, 2 = a donated subtree (level L, index idx)
 };
 // converge's subdivision depth from the transformed curve's flatness (:180-193)
 __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
@@ -385,7 +387,7 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
     // most leaf_level re-derivation splits and one split or leaf test
     s.cap = (uint32_t)(s.leaf_level + 2) << (s.leaf_level + 1);
     s.L = 0; s.base = 0; s.rl = 0; s.idx = 0; s.it = 0; s.rmask = 0;
-    s.fresh = true; s.found = false; s.best = tmax;
+    s.fresh = true; s.found = false; s.best = tmax; s.stg = 0;
 }
 // at a leaf segment: the next call is bez_walk_leaf
 __device__ __forceinline__ bool bez_walk_at_leaf(const BezWalk& s) { return s.fresh && s.L >= s.leaf_level; }
@@ -511,6 +513,41 @@ __device__ __forceinline__ void bez_walk_take(BezWalk& s, const BezierRec& B, co
     s.L = (int)l; s.base = (int)l; s.idx = ridx; s.fresh = false;
 }
 
+// Staged starts (stage B): the curve record's load is issued in one
+// iteration and used in the next (bez_walk_unstage), so its latency overlaps
+// the other lanes' walk steps instead of stalling the wave's refill round.
+// kind 1: the survivor's whole walk (bez_walk_begin); 2: the donated subtree
+// (level l, index ridx) of bez_walk_take.
+__device__ __forceinline__ void bez_walk_stage(BezWalk& s, const BezierRec& B, const double tmax, const int leaf_level,
+                                               const uint8_t kind, const uint32_t l = 0, const uint32_t ridx = 0) {
+    s.c.p0 = mk(B.cp[0], B.cp[1], B.cp[2]);
+    s.c.p1 = mk(B.cp[3], B.cp[4], B.cp[5]);
+    s.c.p2 = mk(B.cp[6], B.cp[7], B.cp[8]);
+    s.c.p3 = mk(B.cp[9], B.cp[10], B.cp[11]);
+    s.w1 = B.w1; s.w2 = B.w2; s.tmax = tmax;
+    s.leaf_level = leaf_level;
+    s.L = (int)l; s.idx = ridx;
+    s.fresh = false;
+    s.stg = kind;
+}
+// the staged start: transform (bezier-transform :99-105, as bez_load) and set
+// the walk up; true if it is already over (a survivor's root culled)
+__device__ __forceinline__ bool bez_walk_unstage(BezWalk& s, const BezRay& R) {
+    Bez4 root;
+    root.p0 = bez_xf(R, s.c.p0.x, s.c.p0.y, s.c.p0.z);
+    root.p1 = bez_xf(R, s.c.p1.x, s.c.p1.y, s.c.p1.z);
+    root.p2 = bez_xf(R, s.c.p2.x, s.c.p2.y, s.c.p2.z);
+    root.p3 = bez_xf(R, s.c.p3.x, s.c.p3.y, s.c.p3.z);
+    const uint8_t kind = s.stg;
+    const int l = s.L;
+    const uint32_t ridx = s.idx;
+    s.stg = 0;
+    if (kind == 1 && bez_culled(root, s.w1, s.tmax)) { s.found = false; return true; }
+    bez_walk_init(s, root, s.w1, s.w2, s.tmax, s.leaf_level);
+    if (kind == 2) { s.L = l; s.base = l; s.idx = ridx; s.fresh = false; }
+    return false;
+}
+
 // Returns true and the curve's t if it reports a hit for t-max `tmax`
 // (bezier.scm:176-214): the root cull, the depth estimate, then the walk.
 __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
@@ -565,6 +602,9 @@ constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per
 #endif
 #ifndef RT_CURVE_FINISH_BATCH
 #define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
+#endif
+#ifndef RT_BEZ_STAGED
+#define RT_BEZ_STAGED 0                // stage B: curve records loaded one iteration before their walks start
 #endif
 #ifndef RT_BEZ_WALK
 #define RT_BEZ_WALK 1                  // stage B node step: 1 = re-derivation in one go, 0 = one split per iteration
@@ -665,6 +705,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         // [31] passes [32] wave iterations [33] busy lane-iterations [34] walk steps [35] re-derived
         // nodes [36] re-derivation splits [37] leaf tests [38] survivors [39] stage B clock (lane 0)
         uint32_t n_it = 0, n_busy = 0, n_step = 0, n_red = 0, n_rsplit = 0, n_leaf = 0;
+        unsigned long long n_clk_refill = 0;          // [45] stage B clock in refill / donation rounds (lane 0)
         const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
 #endif
         const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * (((unsigned long long)(kBezMaxDepth + 3) << (kBezMaxDepth + 2)) + 2ull);
@@ -679,6 +720,9 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                 if (bez_walk_at_leaf(wk)) ++n_leaf;     // lane-iterations at a leaf (tested or waiting)
             }
 #endif
+#ifdef RT_STATS
+            const unsigned long long cr0 = __builtin_amdgcn_s_memtime();
+#endif
             const unsigned long long idle = __ballot(!busy);
             if (cursor < nb && (__popcll(idle) >= kBezRefill || idle == act)) {
                 if (!busy) {
@@ -687,13 +731,18 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                         const uint32_t e = W.sv[i];
                         si = i;
                         W.sz[i] = INFINITY;
+#if RT_BEZ_STAGED
+                        bez_walk_stage(wk, sc.bez[e >> 6], W.cl[e & 63u], W.lev[i], 1);
+                        busy = true;
+#else
                         busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
+#endif
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
             } else if (cursor >= nb && idle != 0ull && idle != act) {
                 // donation round: the candidate queue is empty during stage B, W.q carries the handover
-                const uint32_t pend = busy ? bez_walk_pending(wk) : 0u;
+                const uint32_t pend = (busy && !wk.stg) ? bez_walk_pending(wk) : 0u;
                 const unsigned long long dm = __ballot(pend != 0u);
                 const uint32_t nd = min((uint32_t)__popcll(dm), (uint32_t)__popcll(idle));
                 if (nd) {
@@ -708,13 +757,20 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (!busy && ir < nd) {
                         si = W.q[3 * ir];
                         const uint32_t e = W.sv[si];
+#if RT_BEZ_STAGED
+                        bez_walk_stage(wk, sc.bez[e >> 6], W.cl[e & 63u], W.lev[si], 2, W.q[3 * ir + 1], W.q[3 * ir + 2]);
+#else
                         bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], W.q[3 * ir + 1],
                                       W.q[3 * ir + 2]);
+#endif
                         busy = true;
                     }
                     wave_sync();
                 }
             }
+#ifdef RT_STATS
+            n_clk_refill += __builtin_amdgcn_s_memtime() - cr0;
+#endif
             const unsigned long long bm = __ballot(busy);
             if (bm == 0ull) {
                 if (cursor >= nb) break;
@@ -722,17 +778,21 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             }
             // lanes at a leaf segment wait until enough of them (or every busy lane) are there and
             // then test together; the others split this iteration either way
-            const bool at_leaf = busy && bez_walk_at_leaf(wk);
+            const bool at_leaf = busy && !wk.stg && bez_walk_at_leaf(wk);
             const unsigned long long lm = __ballot(at_leaf);
             bool over = false;
             if (lm != 0ull && (__popcll(lm) >= RT_BEZ_LEAF_PHASE || lm == bm)) {
                 if (at_leaf) over = bez_walk_leaf(wk);
             }
+            if (busy && wk.stg) {
+                over = bez_walk_unstage(wk, W.ray[W.sv[si] & 63u]);
+            } else if (busy && !at_leaf) {
 #if RT_BEZ_WALK == 1
-            if (busy && !at_leaf) over = bez_walk_node(wk);
+                over = bez_walk_node(wk);
 #else
-            if (busy && !at_leaf) over = bez_walk_split(wk);
+                over = bez_walk_split(wk);
 #endif
+            }
             if (over) {
                 if (wk.found)
                     atomicMin((unsigned long long*)&W.sz[si], (unsigned long long)__double_as_longlong(wk.best));
@@ -743,7 +803,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         RT_STAT(33, n_busy); RT_STAT(34, n_step); RT_STAT(35, n_red); RT_STAT(36, n_rsplit); RT_STAT(37, n_leaf);
         if (rank == 0) {
             RT_STAT(31, 1); RT_STAT(32, n_it); RT_STAT(38, nb);
-            RT_STAT(39, __builtin_amdgcn_s_memtime() - clk0);
+            RT_STAT(39, __builtin_amdgcn_s_memtime() - clk0); RT_STAT(45, n_clk_refill);
         }
 #endif
     }
@@ -2470,6 +2530,9 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
+#ifndef RT_TAIL_REFILL
+#define RT_TAIL_REFILL 1               // k_finish: idle lanes that take new paths together
+#endif
 #ifndef RT_FINISH_WAVES
 #define RT_FINISH_WAVES 4             // plain-sphere tails without Perlin / light mixture: 128 VGPRs, 4 waves per SIMD
 #endif                                // (the compiler's choice is 143: 3 waves; the other variants would spill at 128)
@@ -2525,8 +2588,10 @@ __global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(co
     bool active = false, exhausted = false;
     PathRegs p;
     for (;;) {
+        // idle lanes are refilled together once RT_TAIL_REFILL of them wait (or none is active): the
+        // claim atomic and the path loads are round trips the wave pays per refill, not per lane
         const unsigned long long need = __ballot(!active);
-        if (need && !exhausted) {
+        if (need && !exhausted && (__popcll(need) >= RT_TAIL_REFILL || need == ~0ull)) {
             uint32_t base = 0;
             const uint32_t cnt = (uint32_t)__popcll(need);
             const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;

@@ -50,7 +50,7 @@ class RtSceneInfo(ctypes.Structure):
                                               "bvh_solo")] + \
                [(n, ctypes.c_uint32) for n in ("extend_lds_bytes", "extend_lds_blocks", "camera_lds_bytes",
                                                "camera_lds_blocks")] + \
-               [("cus", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+               [("cus", ctypes.c_int32), ("curve_stack", ctypes.c_int32)]
 
 
 # name -> argtypes (restype is always c_int status, except where noted)

@@ -43,7 +43,7 @@ def main():
         "kernel_iters_per_wave": b[23] / waves, "flushes_per_wave": b[25] / waves,
         "kernel_clock_per_iter": b[40] / max(1, b[23]),
         "step1_finish_share": b[42] / max(1, b[40]), "step2_claim_share": b[43] / max(1, b[40]),
-        "step3_bvh_share": b[44] / max(1, b[40]),
+        "step3_bvh_share": b[44] / max(1, b[40]), "stage_b_refill_share": b[45] / max(1, b[40]),
     }
     print(json.dumps(out, indent=1))
 
