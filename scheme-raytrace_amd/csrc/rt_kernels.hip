@@ -347,12 +347,12 @@ __device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay
 // 15 to 5 at C5, but the persistent curve kernel then spills: 120.6 vs 137.8
 // Mrays/s at 4 spp.)
 //
-// Uniform work per call (round 3): a call does ONE split — a descent split
-// (both halves culled) or one level of a right sibling's re-derivation from
-// the root — or, separately, one leaf test (bez_walk_leaf), so the lanes of a
-// wave run the same code in the same iteration.  (One call per node, with
-// the whole re-derivation loop and the leaf test inside, made every wave
-// iteration cost the longest re-derivation among its lanes plus a leaf test.)
+// The walk's calls: bez_walk_split (one split: a descent split, both halves
+// culled, or one level of a right sibling's re-derivation from the root),
+// bez_walk_node (a pending right sibling re-derived in one go, then split)
+// and bez_walk_leaf (a leaf segment's test).  Stage B calls node / leaf, and
+// holds lanes at leaf segments until enough of them test together
+// (RT_BEZ_LEAF_PHASE); the per-lane bezier_test calls split / leaf.
 struct BezWalk {
     Bez4 root, c;
     double best, tmax, w1, w2;
@@ -361,8 +361,6 @@ struct BezWalk {
     uint32_t idx, it, cap;
     uint32_t rmask;                 // bit L: the right sibling of the level-L left half was culled at the split
     bool fresh, found;              // fresh: c is node (L, idx) and passed the cull
-    uint8_t stg;                    // staged (bez_walk_stage): c holds the curve's raw control points; 1 = a
-                                    // survivor's walk, 2 = a donated subtree (level L, index idx)
 };
 // converge's subdivision depth from the transformed curve's flatness (:180-193)
 __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
@@ -387,7 +385,7 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
     // most leaf_level re-derivation splits and one split or leaf test
     s.cap = (uint32_t)(s.leaf_level + 2) << (s.leaf_level + 1);
     s.L = 0; s.base = 0; s.rl = 0; s.idx = 0; s.it = 0; s.rmask = 0;
-    s.fresh = true; s.found = false; s.best = tmax; s.stg = 0;
+    s.fresh = true; s.found = false; s.best = tmax;
 }
 // at a leaf segment: the next call is bez_walk_leaf
 __device__ __forceinline__ bool bez_walk_at_leaf(const BezWalk& s) { return s.fresh && s.L >= s.leaf_level; }
@@ -513,41 +511,6 @@ __device__ __forceinline__ void bez_walk_take(BezWalk& s, const BezierRec& B, co
     s.L = (int)l; s.base = (int)l; s.idx = ridx; s.fresh = false;
 }
 
-// Staged starts (stage B): the curve record's load is issued in one
-// iteration and used in the next (bez_walk_unstage), so its latency overlaps
-// the other lanes' walk steps instead of stalling the wave's refill round.
-// kind 1: the survivor's whole walk (bez_walk_begin); 2: the donated subtree
-// (level l, index ridx) of bez_walk_take.
-__device__ __forceinline__ void bez_walk_stage(BezWalk& s, const BezierRec& B, const double tmax, const int leaf_level,
-                                               const uint8_t kind, const uint32_t l = 0, const uint32_t ridx = 0) {
-    s.c.p0 = mk(B.cp[0], B.cp[1], B.cp[2]);
-    s.c.p1 = mk(B.cp[3], B.cp[4], B.cp[5]);
-    s.c.p2 = mk(B.cp[6], B.cp[7], B.cp[8]);
-    s.c.p3 = mk(B.cp[9], B.cp[10], B.cp[11]);
-    s.w1 = B.w1; s.w2 = B.w2; s.tmax = tmax;
-    s.leaf_level = leaf_level;
-    s.L = (int)l; s.idx = ridx;
-    s.fresh = false;
-    s.stg = kind;
-}
-// the staged start: transform (bezier-transform :99-105, as bez_load) and set
-// the walk up; true if it is already over (a survivor's root culled)
-__device__ __forceinline__ bool bez_walk_unstage(BezWalk& s, const BezRay& R) {
-    Bez4 root;
-    root.p0 = bez_xf(R, s.c.p0.x, s.c.p0.y, s.c.p0.z);
-    root.p1 = bez_xf(R, s.c.p1.x, s.c.p1.y, s.c.p1.z);
-    root.p2 = bez_xf(R, s.c.p2.x, s.c.p2.y, s.c.p2.z);
-    root.p3 = bez_xf(R, s.c.p3.x, s.c.p3.y, s.c.p3.z);
-    const uint8_t kind = s.stg;
-    const int l = s.L;
-    const uint32_t ridx = s.idx;
-    s.stg = 0;
-    if (kind == 1 && bez_culled(root, s.w1, s.tmax)) { s.found = false; return true; }
-    bez_walk_init(s, root, s.w1, s.w2, s.tmax, s.leaf_level);
-    if (kind == 2) { s.L = l; s.base = l; s.idx = ridx; s.fresh = false; }
-    return false;
-}
-
 // Returns true and the curve's t if it reports a hit for t-max `tmax`
 // (bezier.scm:176-214): the root cull, the depth estimate, then the walk.
 __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
@@ -602,12 +565,6 @@ constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per
 #endif
 #ifndef RT_CURVE_FINISH_BATCH
 #define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
-#endif
-#ifndef RT_BEZ_STAGED
-#define RT_BEZ_STAGED 0                // stage B: curve records loaded one iteration before their walks start
-#endif
-#ifndef RT_BEZ_WALK
-#define RT_BEZ_WALK 1                  // stage B node step: 1 = re-derivation in one go, 0 = one split per iteration
 #endif
 constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
 struct BezWave {
@@ -716,7 +673,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             n_busy += busy ? 1u : 0u;
             if (busy) {
                 ++n_step;
-                if (!wk.fresh) { n_red += wk.rl == 0 ? 1u : 0u; n_rsplit += RT_BEZ_WALK == 1 ? (uint32_t)wk.L : 1u; }
+                if (!wk.fresh) { ++n_red; n_rsplit += (uint32_t)wk.L; }
                 if (bez_walk_at_leaf(wk)) ++n_leaf;     // lane-iterations at a leaf (tested or waiting)
             }
 #endif
@@ -731,18 +688,13 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                         const uint32_t e = W.sv[i];
                         si = i;
                         W.sz[i] = INFINITY;
-#if RT_BEZ_STAGED
-                        bez_walk_stage(wk, sc.bez[e >> 6], W.cl[e & 63u], W.lev[i], 1);
-                        busy = true;
-#else
                         busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
-#endif
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
             } else if (cursor >= nb && idle != 0ull && idle != act) {
                 // donation round: the candidate queue is empty during stage B, W.q carries the handover
-                const uint32_t pend = (busy && !wk.stg) ? bez_walk_pending(wk) : 0u;
+                const uint32_t pend = busy ? bez_walk_pending(wk) : 0u;
                 const unsigned long long dm = __ballot(pend != 0u);
                 const uint32_t nd = min((uint32_t)__popcll(dm), (uint32_t)__popcll(idle));
                 if (nd) {
@@ -757,12 +709,8 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (!busy && ir < nd) {
                         si = W.q[3 * ir];
                         const uint32_t e = W.sv[si];
-#if RT_BEZ_STAGED
-                        bez_walk_stage(wk, sc.bez[e >> 6], W.cl[e & 63u], W.lev[si], 2, W.q[3 * ir + 1], W.q[3 * ir + 2]);
-#else
                         bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], W.q[3 * ir + 1],
                                       W.q[3 * ir + 2]);
-#endif
                         busy = true;
                     }
                     wave_sync();
@@ -778,21 +726,13 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             }
             // lanes at a leaf segment wait until enough of them (or every busy lane) are there and
             // then test together; the others split this iteration either way
-            const bool at_leaf = busy && !wk.stg && bez_walk_at_leaf(wk);
+            const bool at_leaf = busy && bez_walk_at_leaf(wk);
             const unsigned long long lm = __ballot(at_leaf);
             bool over = false;
             if (lm != 0ull && (__popcll(lm) >= RT_BEZ_LEAF_PHASE || lm == bm)) {
                 if (at_leaf) over = bez_walk_leaf(wk);
             }
-            if (busy && wk.stg) {
-                over = bez_walk_unstage(wk, W.ray[W.sv[si] & 63u]);
-            } else if (busy && !at_leaf) {
-#if RT_BEZ_WALK == 1
-                over = bez_walk_node(wk);
-#else
-                over = bez_walk_split(wk);
-#endif
-            }
+            if (busy && !at_leaf) over = bez_walk_node(wk);
             if (over) {
                 if (wk.found)
                     atomicMin((unsigned long long*)&W.sz[si], (unsigned long long)__double_as_longlong(wk.best));
@@ -2530,9 +2470,6 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
 // depth 100): one thread per remaining path runs extend + shade in a loop
 // instead of ~100 more wavefront launches with a host sync each.
 // =====================================================================
-#ifndef RT_TAIL_REFILL
-#define RT_TAIL_REFILL 1               // k_finish: idle lanes that take new paths together
-#endif
 #ifndef RT_FINISH_WAVES
 #define RT_FINISH_WAVES 4             // plain-sphere tails without Perlin / light mixture: 128 VGPRs, 4 waves per SIMD
 #endif                                // (the compiler's choice is 143: 3 waves; the other variants would spill at 128)
@@ -2588,10 +2525,8 @@ __global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(co
     bool active = false, exhausted = false;
     PathRegs p;
     for (;;) {
-        // idle lanes are refilled together once RT_TAIL_REFILL of them wait (or none is active): the
-        // claim atomic and the path loads are round trips the wave pays per refill, not per lane
         const unsigned long long need = __ballot(!active);
-        if (need && !exhausted && (__popcll(need) >= RT_TAIL_REFILL || need == ~0ull)) {
+        if (need && !exhausted) {
             uint32_t base = 0;
             const uint32_t cnt = (uint32_t)__popcll(need);
             const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;
