@@ -555,7 +555,13 @@ __device__ unsigned long long g_stats[48];
 // curve's answer does not depend on the t-max it is tested with, beyond
 // being reported only when z <= t-max (see bezier_test), so deferring the
 // tests changes no result.
-constexpr int kBezRefill = 8;         // stage B: idle lanes that take the next survivors together
+#ifndef RT_BEZ_REFILL
+#define RT_BEZ_REFILL 8
+#endif
+constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the next survivors together
+#ifndef RT_BEZ_WAIT_FLUSH
+#define RT_BEZ_WAIT_FLUSH 0            // k_extend_curves: lanes waiting on their curves that force a batch (0 = off)
+#endif
 constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
 #ifndef RT_BEZ_HOLD
 #define RT_BEZ_HOLD 192                // stage B runs once this many root-cull survivors wait (multiple of 64)
@@ -1839,7 +1845,12 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         // 5. batches: root culls at 64 queued candidates, subdivisions in
         //    multiples of 64 (everything once no lane can add candidates)
         const bool more = __ballot(active && (trav || pb < pe)) != 0ull;
-        if (qn >= 64u || (!more && (qn > 0u || svn > 0u))) {
+#if RT_BEZ_WAIT_FLUSH
+        const bool press = __popcll(__ballot(active && !trav && pb >= pe && W.done[lane] != queued)) >= RT_BEZ_WAIT_FLUSH;
+#else
+        constexpr bool press = false;
+#endif
+        if (qn >= 64u || ((!more || press) && (qn > 0u || svn > 0u))) {
 #ifdef RT_STATS
             ++st_flush;
 #endif
@@ -1853,7 +1864,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
             st_clk_a += __builtin_amdgcn_s_memtime() - ca;
 #endif
             qn = 0;
-            const uint32_t nb = more ? (svn >= (uint32_t)RT_BEZ_HOLD ? svn - svn % 64u : 0u) : svn;
+            const uint32_t nb = (more && !press) ? (svn >= (uint32_t)RT_BEZ_HOLD ? svn - svn % 64u : 0u) : svn;
             if (nb > 0u) {
                 W.hz[lane] = INFINITY;
                 W.hkey[lane] = 0ull;
