@@ -559,12 +559,15 @@ __device__ unsigned long long g_stats[48];
 #define RT_BEZ_REFILL 8
 #endif
 constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the next survivors together
+#ifndef RT_BEZ_DONATE
+#define RT_BEZ_DONATE 1                // stage B: idle lanes (at least) that take pending subtrees (0 = no donation)
+#endif
 #ifndef RT_BEZ_WAIT_FLUSH
 #define RT_BEZ_WAIT_FLUSH 0            // k_extend_curves: lanes waiting on their curves that force a batch (0 = off)
 #endif
 constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
 #ifndef RT_BEZ_HOLD
-#define RT_BEZ_HOLD 192                // stage B runs once this many root-cull survivors wait (multiple of 64)
+#define RT_BEZ_HOLD 64                 // stage B runs once this many root-cull survivors wait (multiple of 64)
 #endif
 #ifndef RT_BEZ_LEAF_PHASE
 #define RT_BEZ_LEAF_PHASE 32           // stage B: lanes at a leaf segment that test together
@@ -698,7 +701,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
-            } else if (cursor >= nb && idle != 0ull && idle != act) {
+            } else if (RT_BEZ_DONATE > 0 && cursor >= nb && __popcll(idle) >= RT_BEZ_DONATE && idle != act) {
                 // donation round: the candidate queue is empty during stage B, W.q carries the handover
                 const uint32_t pend = busy ? bez_walk_pending(wk) : 0u;
                 const unsigned long long dm = __ballot(pend != 0u);
