@@ -560,7 +560,7 @@ __device__ unsigned long long g_stats[48];
 #endif
 constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the next survivors together
 #ifndef RT_BEZ_DONATE
-#define RT_BEZ_DONATE 1                // stage B: idle lanes (at least) that take pending subtrees (0 = no donation)
+#define RT_BEZ_DONATE 16               // stage B: idle lanes (at least) that take pending subtrees together (0 = none)
 #endif
 #ifndef RT_BEZ_WAIT_FLUSH
 #define RT_BEZ_WAIT_FLUSH 0            // k_extend_curves: lanes waiting on their curves that force a batch (0 = off)
