@@ -489,10 +489,10 @@ __device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
 // base+1 .. L whose path node is a left half whose right sibling survived its
 // split), as a bit mask by level.
 __device__ __forceinline__ uint32_t bez_walk_pending(const BezWalk& s) {
-    uint32_t pend = 0;
-    for (int l = s.base + 1; l <= s.L; ++l)
-        if (!((s.idx >> (s.L - l)) & 1u) && !((s.rmask >> l) & 1u)) pend |= 1u << l;
-    return pend;
+    // level l's path node is a left half iff bit L - l of idx is 0: bit-reverse the complement so that
+    // bit becomes bit l, keep levels base+1 .. L, drop the siblings culled at their split
+    const uint32_t left = __builtin_bitreverse32(~s.idx & ((1u << s.L) - 1u)) >> (31 - s.L);
+    return left & ~((2u << s.base) - 1u) & ~s.rmask;
 }
 // Hand the shallowest pending right sibling to another lane: returns its
 // (level, index); this walk will skip it.
