@@ -104,6 +104,7 @@ struct Lane {
     // the chunk in flight
     enum State { IDLE, RUNNING, DONE } state = IDLE;
     int chunk = -1, depth = 0;
+    int index = 0;                             // the lane's position in Context::lanes
     bool fused_camera = false;                 // depth 0 runs k_camera (no raygen pass)
     uint32_t n = 0, S = 0;
     uint64_t seq = 0;                          // enqueue order of the pending iteration
@@ -1019,7 +1020,7 @@ int commit_scene(Scene* s, int world) {
             HIPCHK(hipGetDevice(&dev));
             HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             d.ovf_lanes = (uint32_t)std::max(cus, 1) * 2048u;     // any resident grid of 256-thread blocks
-            HIPCHK(s->d_stk_ovf.ensure((size_t)d.ovf_lanes * (size_t)(stack4 - lane_stack) * sizeof(uint32_t)));
+            HIPCHK(s->d_stk_ovf.ensure((size_t)kLanes * d.ovf_lanes * (size_t)(stack4 - lane_stack) * sizeof(uint32_t)));
             d.stk_ovf = s->d_stk_ovf.as<uint32_t>();
         }
     }
@@ -1278,6 +1279,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     HIPCHK(hipEventRecord(ev_in, stream));
     for (int li = 0; li < nlanes; ++li) {
         if (!c->lanes[li]) c->lanes[li].reset(new Lane());
+        c->lanes[li]->index = li;
         Lane& L = *c->lanes[li];
         if (!L.stream) HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
         if (!L.ev_cnt) HIPCHK(hipEventCreateWithFlags(&L.ev_cnt, hipEventDisableTiming));
@@ -1348,10 +1350,14 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         else if (L.depth > 0 && s->ext_lds)     // every ray of a depth >= 1 launch has time +0.0
             HIPCHK(launch_extend_lds(s->dev, L.rp, *L.cur, L.view, L.n, hit, (uint32_t)shard_cap,
                                      cnt, s->ext_lds_blocks, L.seg_tail.as<unsigned long long>() + 2, L.stream));
-        else
-            HIPCHK(launch_extend(s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
+        else {
+            // the curve walk's stack overflow area: one region per render lane (lanes run concurrently)
+            DevScene dl = s->dev;
+            if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lane_stack);
+            HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
                                  reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1), L.stream));
+        }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
         for (int mt = 0; mt < 4; ++mt) {

@@ -142,7 +142,8 @@ struct DevScene {
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     // BVH4 of the same tree (curve trees only, else nullptr): its walk pushes up to three children per
     // node, stack4 entries at most; entries past the LDS stack (lane_stack) go to stk_ovf, stack4 -
-    // lane_stack words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g)
+    // lane_stack words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g);
+    // the buffer holds one such region per render lane and each launch gets its lane's (rt_api.cpp)
     const BvhNode4* bvh4;  int32_t n_bvh4;
     int32_t bvh4_root, stack4;
     uint32_t* stk_ovf;     uint32_t ovf_lanes;
