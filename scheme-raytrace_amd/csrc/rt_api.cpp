@@ -1015,12 +1015,15 @@ int commit_scene(Scene* s, int world) {
         d.n_bvh4 = (int)bvh4.size();
         d.bvh4_root = bvh4_root;
         d.stack4 = stack4;
-        if (stack4 > lane_stack) {                   // the walk's deepest stacks spill past the LDS columns
+        // RTAMD_CURVE_LDS_STACK (tests): fewer LDS entries, so the walk exercises its overflow area
+        const char* ce = std::getenv("RTAMD_CURVE_LDS_STACK");
+        d.lds4 = ce ? std::max(1, std::min(lane_stack, std::atoi(ce))) : lane_stack;
+        if (stack4 > d.lds4) {                       // the walk's deepest stacks spill past the LDS columns
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
             HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             d.ovf_lanes = (uint32_t)std::max(cus, 1) * 2048u;     // any resident grid of 256-thread blocks
-            HIPCHK(s->d_stk_ovf.ensure((size_t)kLanes * d.ovf_lanes * (size_t)(stack4 - lane_stack) * sizeof(uint32_t)));
+            HIPCHK(s->d_stk_ovf.ensure((size_t)kLanes * d.ovf_lanes * (size_t)(stack4 - d.lds4) * sizeof(uint32_t)));
             d.stk_ovf = s->d_stk_ovf.as<uint32_t>();
         }
     }
@@ -1353,7 +1356,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         else {
             // the curve walk's stack overflow area: one region per render lane (lanes run concurrently)
             DevScene dl = s->dev;
-            if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lane_stack);
+            if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lds4);
             HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
                                  reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1), L.stream));

@@ -141,11 +141,12 @@ struct DevScene {
     float bvh_pad;                                 // the margin baked into the f32 boxes (diagnostic)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     // BVH4 of the same tree (curve trees only, else nullptr): its walk pushes up to three children per
-    // node, stack4 entries at most; entries past the LDS stack (lane_stack) go to stk_ovf, stack4 -
-    // lane_stack words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g);
+    // node, stack4 entries at most; entries past the LDS stack (lds4) go to stk_ovf, stack4 - lds4
+    // words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g);
     // the buffer holds one such region per render lane and each launch gets its lane's (rt_api.cpp)
     const BvhNode4* bvh4;  int32_t n_bvh4;
     int32_t bvh4_root, stack4;
+    int32_t lds4;                                  // the walk's stack entries in LDS (lane_stack; tests lower it)
     uint32_t* stk_ovf;     uint32_t ovf_lanes;
     // Time-0 tree over the same primitives (nullptr = none): every moving
     // sphere frozen at center(0), so rays with time +0.0 (all scattered rays,

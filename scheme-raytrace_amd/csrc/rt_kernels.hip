@@ -1646,7 +1646,6 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     __shared__ BezWave s_bw[4];
     BezWave& W = s_bw[threadIdx.x >> 6];
     uint32_t* lstk = s_lstack + threadIdx.x;
-    const int lmax = sc.lane_stack;
     const uint32_t stride = blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
     const QMap qm = qmap(in);
@@ -1661,18 +1660,19 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     BoxRay br{};
     BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
     int sp = 0, pb = 0, pe = 0;
-    // the walk's stack: LDS column for the first lmax entries, the global overflow area past them
+    // the walk's stack: LDS column for the first lds4 entries, the global overflow area past them
+    const int lds4 = sc.lds4;                       // <= lane_stack, the column's allocated depth
     const uint32_t ovf_lane = blockIdx.x * 256u + threadIdx.x;
-    const int scap = max(lmax, sc.stack4);          // commit_scene's bound on the walk's stack
+    const int scap = max(lds4, sc.stack4);          // commit_scene's bound on the walk's stack
     auto push = [&](const int32_t e) {
         if (sp >= scap) { raise_fault(RT_FAULT_PATH); return; }
-        if (sp < lmax) lstk[sp * stride] = (uint32_t)e;
-        else sc.stk_ovf[(size_t)(sp - lmax) * sc.ovf_lanes + ovf_lane] = (uint32_t)e;
+        if (sp < lds4) lstk[sp * stride] = (uint32_t)e;
+        else sc.stk_ovf[(size_t)(sp - lds4) * sc.ovf_lanes + ovf_lane] = (uint32_t)e;
         ++sp;
     };
     auto pop = [&]() -> int32_t {
         --sp;
-        return (int32_t)(sp < lmax ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lmax) * sc.ovf_lanes + ovf_lane]);
+        return (int32_t)(sp < lds4 ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lds4) * sc.ovf_lanes + ovf_lane]);
     };
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
     // a ray takes at most one step per node / leaf and one queue step per two curves: bound its

@@ -222,3 +222,23 @@ def test_few_curves_among_spheres_large_launch(gpu_ctx, oracle_mod, monkeypatch)
     print("few curves among spheres: segments %d, rows %d..%d vs oracle rms=%.3e max=%.3e pixels>1e-9: %d/%d"
           % (st.segments, y0, y0 + rows - 1, rms, dmax, nbad, npx))
     assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
+
+
+def test_curve_walk_stack_overflow_bitwise(gpu_ctx, monkeypatch):
+    """The curve kernel's BVH4 walk pushes up to three children per node;
+    commit_scene bounds its stack (rt_scene_info.curve_stack) and entries past
+    the LDS column go to a per-lane overflow area in HBM, one region per render
+    lane.  With the LDS column cut to one entry (RTAMD_CURVE_LDS_STACK=1) every
+    deeper push takes that path, on two render lanes: the image must not
+    change by a bit."""
+    nx, ny, spp = 96, 64, 4
+    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=2, RTAMD_MAX_PATHS=nx * ny)
+    base = np.zeros(nx * ny * 3)
+    h = gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, base)
+    info, st = gpu.scene_info(h), gpu.stats(h)
+    assert info["curve_stack"] > 4 and st.lanes == 2 and st.finish_paths == 0
+    monkeypatch.setenv("RTAMD_CURVE_LDS_STACK", "1")
+    low = np.zeros_like(base)
+    gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, low)
+    print("curve walk stack: bound %d, LDS entries 1 vs %d" % (info["curve_stack"], info["tree_depth"]))
+    assert np.array_equal(base, low)
