@@ -565,7 +565,10 @@ constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the
 #ifndef RT_BEZ_WAIT_FLUSH
 #define RT_BEZ_WAIT_FLUSH 0            // k_extend_curves: lanes waiting on their curves that force a batch (0 = off)
 #endif
-constexpr int kBezQ = 64 + 2 * 64;    // candidates: < 64 before a step, + 2 per lane per step
+#ifndef RT_BEZ_QFLUSH
+#define RT_BEZ_QFLUSH 48               // k_extend_curves: queued candidates that trigger a batch (stage A)
+#endif
+constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 2 * 64;   // < the trigger before a step, + 2 per lane per step
 #ifndef RT_BEZ_HOLD
 #define RT_BEZ_HOLD 64                 // stage B runs once this many root-cull survivors wait (multiple of 64)
 #endif
@@ -1854,7 +1857,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
 #else
         constexpr bool press = false;
 #endif
-        if (qn >= 64u || ((!more || press) && (qn > 0u || svn > 0u))) {
+        if (qn >= (uint32_t)RT_BEZ_QFLUSH || ((!more || press) && (qn > 0u || svn > 0u))) {
 #ifdef RT_STATS
             ++st_flush;
 #endif
