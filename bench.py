@@ -16,10 +16,22 @@ into the frame (rtamd.dist.gather_frame; the pixels are disjoint, so the
 frame is bit-identical to one GPU's).  Total work per step is fixed:
 "scaling": "strong".
 
-Parity (the metric's "per-pixel RMS vs ref"): after the timed steps rank 0
-times the oracle on a 64-row band of the frame at the top sample indices
-(cpu_baseline) and renders the same band and passes on the GPU with the
-production schedule; rms_vs_oracle / max_abs / pixels_gt_1e-9 compare them.
+Each step also resolves the frame to bytes on the device (rt_resolve_u8_device,
+main.scm:481-491), after the gather when N > 1.
+
+Parity (the metric's "per-pixel RMS vs ref"), at every N, after the timed
+steps on rank 0: (1) `parity`: the oracle renders a 64-row band at the top
+sample indices (at N=1 this is also the timed cpu_baseline) and the GPU renders
+the same band and passes with the production schedule; (2) `parity_frame`:
+rows of the last timed frame itself (gathered from every rank when N > 1)
+against the oracle's render of those rows with every pass.
+
+Roofline: `roofline` is the closest-hit kernels' own HBM fraction (one render
+lane, HIP events on the lane's stream; with two lanes in the timed region it
+comes from one extra untimed single-lane frame, and the overlapped figure is
+`roofline_two_lane`); `roofline_frame` is the whole path's algorithmic bytes
+per frame over ms_per_step.  PMC-derived `traffic` / `valu` / `valu_issue`
+come from profiles/pmc_*.json only when those carry this rt_kernels.hip's hash.
 """
 import argparse
 import json
@@ -74,24 +86,21 @@ def shade_bytes(hits_d0, hits, survivors):
     return (76 * hits_d0 + 96 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
 
 
-def shade_roofline(st, note, scene):
-    if not st or not st.extend_launches or st.ms_shade <= 0 or not (st.shade_hits_d0 + st.shade_hits):
+def shade_roofline(ms_shade, launches, hits_d0, hits, survivors, note, scene):
+    """The shade phase (one iteration's per-material k_shade launches, HIP
+    events around them) against the HBM roofline."""
+    if not launches or ms_shade <= 0 or not (hits_d0 + hits):
         return None
-    b = shade_bytes(st.shade_hits_d0, st.shade_hits, st.shade_survivors)
-    ach = b / (st.ms_shade * 1e-3) / 1e9
-    hpl = (st.shade_hits_d0 + st.shade_hits) / st.extend_launches
-    traffic = None                      # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
-    pmc = os.path.join(ROOT, "profiles", "pmc_shade.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            pm = json.load(f)
-        if pm.get("scene") == scene and pm.get("bytes_per_hit"):
-            traffic = round(pm["bytes_per_hit"] * hpl)
+    b = shade_bytes(hits_d0, hits, survivors)
+    ach = b / (ms_shade * 1e-3) / 1e9
+    hpl = (hits_d0 + hits) / launches
+    pm = load_pmc("pmc_shade.json", scene)      # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
+    traffic = round(pm["bytes_per_hit"] * hpl) if pm and pm.get("bytes_per_hit") else None
     return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
             "kernel": "k_shade<material> (one iteration's launches)",
-            "bytes_per_launch": round(b / st.extend_launches), "hits_per_launch": round(hpl),
-            "avg_launch_ms": round(st.ms_shade / st.extend_launches, 4), "note": note}
+            "bytes_per_launch": round(b / launches), "hits_per_launch": round(hpl),
+            "avg_launch_ms": round(ms_shade / launches, 4), "note": note}
 
 
 def scene_device(info):
@@ -120,6 +129,7 @@ def parse():
                    help="skip the CPU baseline and with it the band parity check (both need the oracle)")
     p.add_argument("--no-profile-events", action="store_true")
     p.add_argument("--no-isolated", action="store_true", help="skip the single-lane profiling frame")
+    p.add_argument("--lanes", type=int, default=0, help="render lanes (RT_OPT_LANES); 0 = the library's choice")
     return p.parse_args()
 
 
@@ -161,21 +171,11 @@ def band_rows(ny):
     return max(0, ny // 3 - rows // 2), rows
 
 
-def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
-    """The oracle (C f64 restatement, OpenMP over pixels) timed on the host:
-    (1) on the process's whole CPU share, on a 64-row band of the frame at the
-        top sample indices (passes spp-P .. spp-1, P sized to ~budget_s); its
-        accumulator is also the parity reference for the GPU's band;
-    (2) on one thread, rows of the same band at pass spp-1 (~budget_s/3);
-    (3) config C1 (cover scene 200x100x8 spp) in full, all threads and one.
-    Returns (cpu_baseline dict, band reference)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def oracle_band(o, scene, nx, ny, spp, seed, budget_s, T):
+    """The oracle on rows y0..y0+63 at the top sample indices (passes spp-P ..
+    spp-1, P sized to ~budget_s on T threads).  Returns (ref, segments,
+    seconds, per-row-pass seconds)."""
     import numpy as np
-    import oracle  # cpu_baseline leg only
-    from rtamd import scenes
-    host = host_cpu()
-    T = host["threads_used"]
-    o = oracle.build_scene(scene)
     y0, rows = band_rows(ny)
     lo, hi = y0 * nx, (y0 + rows) * nx
     # calibrate: one pass over 8 rows (after a zero-pixel call that builds the oracle's trees)
@@ -189,6 +189,23 @@ def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
     t = time.perf_counter()
     _, segs = o.render(nx, ny, spp - P, P, seed, acc, lo, hi, T)
     t_all = time.perf_counter() - t
+    return {"acc": acc, "y0": y0, "rows": rows, "spp_begin": spp - P, "passes": P}, segs, t_all, per_row_pass
+
+
+def cpu_baseline(o, scene, nx, ny, spp, seed, budget_s, host):
+    """The oracle (C f64 restatement, OpenMP over pixels) timed on the host:
+    (1) on the process's whole CPU share, on a 64-row band of the frame at the
+        top sample indices (oracle_band); its accumulator is also the parity
+        reference for the GPU's band;
+    (2) on one thread, rows of the same band at pass spp-1 (~budget_s/3);
+    (3) config C1 (cover scene 200x100x8 spp) in full, all threads and one.
+    Returns (cpu_baseline dict, band reference, per-row-pass seconds)."""
+    import numpy as np
+    from rtamd import scenes
+    T = host["threads_used"]
+    ref, segs, t_all, per_row_pass = oracle_band(o, scene, nx, ny, spp, seed, budget_s, T)
+    y0, rows, P = ref["y0"], ref["rows"], ref["passes"]
+    lo = y0 * nx
     # one thread: the band row by row, pass spp-1 then spp-2 ..., until ~budget/3
     one = np.zeros(nx * ny * 3)
     t1, segs1, done = 0.0, 0, 0
@@ -200,6 +217,7 @@ def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
         segs1 += sg
         done += 1
     # C1 in full (200x100, 8 passes, seed 0x5EED0001)
+    import oracle  # cpu_baseline leg only
     c1 = oracle.build_scene(scenes.random_scene(200, 100))
     c1_rates = {}
     for th in (T, 1):
@@ -219,7 +237,31 @@ def cpu_baseline(scene, nx, ny, spp, seed, budget_s):
                        "threads": {str(T): round(c1_rates[T][0], 3), "1": round(c1_rates[1][0], 4)},
                        "unit": "Mrays/s", "segments": c1_rates[1][1]},
            "host": host}
-    return out, {"acc": acc, "y0": y0, "rows": rows, "spp_begin": spp - P, "passes": P}
+    return out, ref, per_row_pass
+
+
+def frame_rows_parity(o, frame_np, nx, ny, spp, seed, per_row_pass, budget_s, T):
+    """Rows of the benchmarked frame itself (rank 0's, after the gather when
+    N > 1: every rank's tiles cross a row) against the oracle's render of the
+    same rows with every pass 0..spp-1.  Rows: as many as ~budget_s of oracle
+    time allows (1..8), centred in the frame."""
+    import numpy as np
+    rows = int(max(1, min(8, budget_s / max(1e-9, per_row_pass * spp))))
+    y0 = max(0, ny // 2 - rows // 2)
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    ref = np.zeros(nx * ny * 3)
+    t = time.perf_counter()
+    o.render(nx, ny, 0, spp, seed, ref, lo, hi, T)
+    dt = time.perf_counter() - t
+    got = frame_np[3 * lo:3 * hi] / spp
+    exp = ref[3 * lo:3 * hi] / spp
+    d = np.abs(got - exp)
+    rms = float(np.sqrt(np.mean(d ** 2)))
+    return {"rms_vs_oracle": rms, "max_abs": float(d.max()),
+            "pixels_gt_1e-9": int((d.reshape(-1, 3).max(axis=1) > 1e-9).sum()), "pixels": int(d.size // 3),
+            "tolerance_rms": 1e-4, "pass": bool(rms <= 1e-4), "rows": "%d..%d" % (y0, y0 + rows - 1),
+            "passes": "0..%d" % (spp - 1), "oracle_s": round(dt, 1),
+            "note": "rows of the last timed frame (the gathered frame on rank 0) vs the oracle, all passes"}
 
 
 def gpu_band_parity(scene, nx, ny, seed, ref, h, ctx):
@@ -264,11 +306,63 @@ SCENE_DATA = {
 }
 
 
+def kernel_sha16():
+    """Hash of the kernel source the PMC summaries under profiles/ must carry
+    (tools/pmc_report.py stamps them) for bench.py to use their counters."""
+    import hashlib
+    with open(os.path.join(ROOT, "scheme-raytrace_amd", "csrc", "rt_kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_pmc(name, scene):
+    """profiles/<name> if it was measured on this scene with these kernels, else None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pm = json.load(f)
+    if pm.get("scene") != scene or pm.get("kernel_sha16") != kernel_sha16():
+        return None
+    return pm
+
+
+def extend_roofline(segs, tail_segs, paths, launches, ms_ext, pm, kernels, note):
+    """The closest-hit kernels' HBM roofline: algorithmic bytes per launch over
+    the average launch duration (HIP events on the lane's stream)."""
+    if not launches or ms_ext <= 0:
+        return None
+    wf_segs = segs - tail_segs
+    rays_per_launch = wf_segs / launches
+    avg_ms = ms_ext / launches
+    bytes_per_launch = extend_bytes(wf_segs, paths) / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": round(pm["bytes_per_segment"] * rays_per_launch) if pm else None,
+            "kernel": kernels, "bytes_per_launch": round(bytes_per_launch),
+            "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+            "note": note}
+
+
+# Algorithmic HBM bytes of the rest of the frame (roofline_frame): a tail
+# path (k_finish) reads its ray + path records once (80 B) and writes its
+# sample (24 B); the accumulate reads every sample (24 B) and reads + writes
+# each pixel's running sum once per chunk (48 B); the resolve reads the sum
+# (24 B) and writes the bytes (3 B) per pixel.
+TAIL_BYTES_PER_PATH = 80 + 24
+
+
+def frame_bytes(segs, tail_segs, paths, sh_d0, sh, sh_surv, finish_paths, npix, chunks):
+    return {"extend": extend_bytes(segs - tail_segs, paths), "shade": shade_bytes(sh_d0, sh, sh_surv),
+            "tail": TAIL_BYTES_PER_PATH * finish_paths, "accumulate": 24 * paths + 48 * npix * chunks,
+            "resolve": 27 * npix}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -281,28 +375,45 @@ def main():
     # multi-process flow on fewer GPUs than ranks (ranks share devices, the gather goes
     # through host memory); it is never the measured configuration.
     backend = os.environ.get("RTAMD_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
-    torch.cuda.set_device(local)
+    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(backend)
     nx, ny, spp = a.nx, a.ny, a.spp
     scene = scenes.SCENES[a.scene](nx, ny)
-    ctx = gpu.default_context(local)
+    ctx = gpu.default_context(device)
+    if a.lanes:
+        ctx.set_option("lanes", a.lanes)
     h = gpu.upload(scene, ctx)                      # one-time scene upload (not timed)
     call("rt_set_profiling", h, 0 if a.no_profile_events else 1)
     # world == 1: the frame accumulator; world > 1: this rank's compact shard (its tiles only), gathered
-    # onto rank 0 over RCCL at frame end (rtamd.dist.gather_frame)
+    # onto rank 0 over RCCL at frame end (rtamd.dist.gather_frame).  Rank 0 resolves the frame to bytes
+    # (main.scm:481-491) inside the step.
     frame = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda") if world == 1 or rank == 0 else None
-    local = torch.zeros(rdist.local_size(nx, ny, rank, world), dtype=torch.float64, device="cuda") \
+    shard = torch.zeros(rdist.local_size(nx, ny, rank, world), dtype=torch.float64, device="cuda") \
         if world > 1 else None
+    image = torch.zeros(nx * ny * 3, dtype=torch.uint8, device="cuda") if frame is not None else None
 
     def step():
-        (frame if world == 1 else local).zero_()
-        rdist.render_frame(scene, nx, ny, 0, spp, a.seed, rank, world, local=local, frame=frame, ctx=ctx)
-        return gpu.stats(h)
+        t0 = time.perf_counter()
+        stream = torch.cuda.current_stream().cuda_stream
+        if world == 1:
+            frame.zero_()
+            gpu.render_device(scene, nx, ny, 0, spp, a.seed, frame.data_ptr(), stream=stream, ctx=ctx)
+        else:
+            shard.zero_()
+            gpu.render_shard_device(scene, nx, ny, 0, spp, a.seed, rank, world, shard.data_ptr(), stream=stream,
+                                    ctx=ctx)
+        t1 = time.perf_counter()                    # the render call returns with its streams drained
+        if world > 1:
+            rdist.gather_frame(shard, nx, ny, rank, world, out=frame)
+        if frame is not None:
+            gpu.resolve_u8_device(frame.data_ptr(), nx, ny, spp, image.data_ptr(), stream=stream, ctx=ctx)
+        torch.cuda.synchronize()
+        return gpu.stats(h), t1 - t0, time.perf_counter() - t1
 
     def progress(msg):                 # a line per frame: long configurations (C5) take a minute per frame
         if rank == 0:
@@ -319,11 +430,15 @@ def main():
     segs = paths = 0
     ms_ext = ms_shade = ms_fin = 0.0
     launches = 0
-    tail_segs = 0
+    tail_segs = finish_paths = chunks = 0
     sh_d0 = sh = sh_surv = 0
+    t_render = t_gather = 0.0
+    lanes = 0
     for k in range(a.steps):
-        s = step()
+        s, tr, tg = step()
         progress("timed frame %d/%d" % (k + 1, a.steps))
+        t_render += tr
+        t_gather += tg
         segs += s.segments
         paths += s.paths
         ms_ext += s.ms_extend
@@ -331,6 +446,9 @@ def main():
         launches += s.extend_launches
         ms_fin += s.ms_finish
         tail_segs += s.segments - s.extend_rays
+        finish_paths += s.finish_paths
+        chunks += s.chunks
+        lanes = s.lanes
         sh_d0 += s.shade_hits_d0
         sh += s.shade_hits
         sh_surv += s.shade_survivors
@@ -338,96 +456,104 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # One more (untimed) frame with a single render lane: the overlapped lanes
-    # of the timed steps run two chunks' kernels concurrently, so a kernel's
-    # event-bracketed duration there includes its neighbour's work.  This
-    # frame gives each kernel's duration with the chip to itself.
+    last_frame = frame.cpu().numpy() if frame is not None else None
+    # The timed frames keep two render lanes in flight (one for curve scenes): a kernel's
+    # event-bracketed duration there includes the other lane's concurrent kernels.  One more
+    # (untimed) frame with a single lane gives each kernel its own duration; with one lane
+    # already, the timed region's events are the kernels' own.
     iso = None
-    if not a.no_profile_events and not a.no_isolated:
-        os.environ["RTAMD_LANES"] = "1"
-        try:
-            iso = step()
-        finally:
-            del os.environ["RTAMD_LANES"]
+    if not a.no_profile_events and not a.no_isolated and lanes > 1:
+        with ctx.options(lanes=1):
+            iso = step()[0]
         progress("single-lane profiling frame")
     red_dev = "cpu" if backend == "gloo" else "cuda"
     tot = torch.tensor([segs, paths], dtype=torch.float64, device=red_dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    per_rank = torch.tensor([t_render, t_gather], dtype=torch.float64, device=red_dev)
+    ranks = [per_rank.clone() for _ in range(world)]
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_gather(ranks, per_rank)
     segs_all, paths_all = float(tot[0]), float(tot[1])
     elapsed = float(tmax[0])
     if rank == 0:
         value = segs_all / elapsed / 1e6
-        roof = None
-        valu = None
-        valu_issue = None
-        roof_iso = None
         ext_kernels = extend_kernels(a.scene, gpu.scene_info(h))
-        pm = None                       # PMC bytes / issue counters of the extend kernels (tools/profile_round.sh)
-        pmc = os.path.join(ROOT, "profiles", "pmc_extend.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("scene") != a.scene or not pm.get("bytes_per_segment"):
-                pm = None
-        if iso is not None and iso.extend_launches and iso.ms_extend > 0:
-            bpl = extend_bytes(iso.extend_rays, iso.paths) / iso.extend_launches
-            ams = iso.ms_extend / iso.extend_launches
-            ach = bpl / (ams * 1e-3) / 1e9
-            roof_iso = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 5), "kernel": ext_kernels,
-                        "bytes_per_launch": round(bpl), "rays_per_launch": round(iso.extend_rays / iso.extend_launches),
-                        "avg_launch_ms": round(ams, 4),
-                        "traffic": round(pm["bytes_per_segment"] * iso.extend_rays / iso.extend_launches) if pm else None,
-                        "note": "one extra untimed frame with a single render lane (no concurrent kernels)"}
-        if launches and ms_ext > 0:
-            # wavefront extend launches only (the depth tail runs in k_finish)
-            wf_segs = segs - tail_segs
-            rays_per_launch = wf_segs / launches
-            avg_ms = ms_ext / launches
-            bytes_per_launch = extend_bytes(wf_segs, paths) / launches
-            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-            traffic = None
-            if pm:
-                traffic = round(pm["bytes_per_segment"] * rays_per_launch)
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": ext_kernels, "bytes_per_launch": round(bytes_per_launch),
-                    "rays_per_launch": round(rays_per_launch), "avg_launch_ms": round(avg_ms, 4),
-                    "note": "timed region; render lanes overlap, so launch durations include concurrent kernels"}
-            if pm and pm.get("valu_busy") is not None:
-                # share of SIMD cycles issuing VALU over the extend kernels (rocprofv3 VALUBusy, one bench frame):
-                # the issue-side roofline of these VALU / latency-bound kernels
-                valu_issue = {"bound": "valu_issue", "achieved": round(pm["valu_busy"] / 100.0, 4), "peak": 1.0,
-                              "unit": "fraction of SIMD cycles issuing VALU",
-                              "frac": round(pm["valu_busy"] / 100.0, 4),
-                              "lane_utilization": round(pm["valu_lane_utilization"] / 100.0, 4),
-                              "lds_busy": round(pm["lds_busy"] / 100.0, 4),
-                              "lds_bank_conflict_ratio": round(pm["lds_bank_conflict_ratio"], 4),
-                              "wait_share": round(pm["wait_share"], 4),
-                              "valu_instr_per_segment": round(pm["valu_instr_per_segment"], 2),
-                              "source": "profiles/pmc_extend.json (%s)" % pm.get("config", "")}
-            if pm and pm.get("f64_flops_per_segment"):
-                tf = pm["f64_flops_per_segment"] * rays_per_launch / (avg_ms * 1e-3) / 1e12
-                valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
-                        "f64_flops_per_segment": round(pm["f64_flops_per_segment"], 1),
-                        "note": "issued f64 lane-ops from SQ_INSTS_VALU_{ADD,MUL,FMA(x2),TRANS}_F64 x 64"}
+        pm = load_pmc("pmc_extend.json", a.scene)   # PMC counters of these kernels (tools/profile_round.sh)
+        two_lane = None
+        if iso is not None:
+            roof = extend_roofline(iso.segments, iso.segments - iso.extend_rays, iso.paths,
+                                   iso.extend_launches, iso.ms_extend, pm, ext_kernels,
+                                   "single render lane: one extra untimed frame right after the timed ones "
+                                   "(HIP events on the lane's stream, nothing concurrent)")
+            two_lane = extend_roofline(segs, tail_segs, paths, launches, ms_ext, pm, ext_kernels,
+                                       "timed region, %d render lanes overlapped: launch durations include the "
+                                       "other lane's kernels" % lanes)
+        else:
+            roof = extend_roofline(segs, tail_segs, paths, launches, ms_ext, pm, ext_kernels,
+                                   "timed region, one render lane (HIP events on the lane's stream)")
+        valu = valu_issue = None
+        if pm and roof and pm.get("valu_busy") is not None:
+            # share of SIMD cycles issuing VALU over the extend kernels (rocprofv3 VALUBusy, one bench frame):
+            # the issue-side roofline of these VALU / latency-bound kernels
+            valu_issue = {"bound": "valu_issue", "achieved": round(pm["valu_busy"] / 100.0, 4), "peak": 1.0,
+                          "unit": "fraction of SIMD cycles issuing VALU",
+                          "frac": round(pm["valu_busy"] / 100.0, 4),
+                          "lane_utilization": round(pm["valu_lane_utilization"] / 100.0, 4),
+                          "lds_busy": round(pm["lds_busy"] / 100.0, 4),
+                          "lds_bank_conflict_ratio": round(pm["lds_bank_conflict_ratio"], 4),
+                          "wait_share": round(pm["wait_share"], 4),
+                          "valu_instr_per_segment": round(pm["valu_instr_per_segment"], 2),
+                          "source": "profiles/pmc_extend.json (%s, kernels %s)" % (pm.get("config", ""),
+                                                                                   pm["kernel_sha16"])}
+        if pm and roof and pm.get("f64_flops_per_segment"):
+            tf = pm["f64_flops_per_segment"] * roof["rays_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
+            valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+                    "f64_flops_per_segment": round(pm["f64_flops_per_segment"], 1),
+                    "note": "issued f64 lane-ops from SQ_INSTS_VALU_{ADD,MUL,FMA(x2),TRANS}_F64 x 64"}
+        # the whole path's algorithmic bytes per frame over the frame time: north_star's path-level figure
+        fb = frame_bytes(segs, tail_segs, paths, sh_d0, sh, sh_surv, finish_paths, nx * ny, chunks)
+        fb_step = {k: v / a.steps for k, v in fb.items()}
+        frame_ach = sum(fb.values()) / elapsed / 1e9 if world == 1 else None
+        roof_frame = None
+        if frame_ach is not None:
+            roof_frame = {"bound": "hbm", "achieved": round(frame_ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(frame_ach / HBM_PEAK_GBS, 5),
+                          "bytes_per_step": {k: round(v) for k, v in fb_step.items()},
+                          "note": "algorithmic bytes of every kernel of the frame (extend + shade + tail + "
+                                  "accumulate + resolve) / ms_per_step"}
+        render_s = [float(r[0]) / a.steps for r in ranks]
+        gather_s = [float(r[1]) / a.steps for r in ranks]
         out = {
-            "metric": metric_for(a.scene, nx, ny, spp), "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "metric": metric_for(a.scene, nx, ny, spp), "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: %s; path RNG seed %#x" % (SCENE_DATA.get(a.scene, a.scene + " scene"), a.seed),
-            "config": {"workload": "%s: %s scene %dx%dx%dspp, one full frame per step"
-                                   % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp),
+            "config": {"workload": "%s: %s scene %dx%dx%dspp, one full frame per step (render + %sresolve)"
+                                   % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx, ny, spp,
+                                      "gather + " if world > 1 else ""),
                        "scene": a.scene, "nx": nx, "ny": ny, "spp": spp,
                        "parallelism": ("tile-shard%d" % world if world > 1 else "single") +
                                       ("" if world == 1 or backend == "nccl" else " (%s rehearsal)" % backend)},
-            "roofline": roof, "roofline_isolated": roof_iso, "valu": valu, "valu_issue": valu_issue,
-            "roofline_shade_isolated": shade_roofline(iso, "single render lane frame, as roofline_isolated", a.scene),
+            "roofline": roof, "roofline_two_lane": two_lane, "roofline_frame": roof_frame,
+            "valu": valu, "valu_issue": valu_issue,
+            "roofline_shade": (shade_roofline(iso.ms_shade, iso.extend_launches, iso.shade_hits_d0, iso.shade_hits,
+                                              iso.shade_survivors, "single render lane frame, as roofline", a.scene)
+                               if iso is not None else
+                               shade_roofline(ms_shade, launches, sh_d0, sh, sh_surv, "timed region, one render lane",
+                                              a.scene)),
+            "pmc_source": ("profiles/pmc_extend.json (kernels %s)" % pm["kernel_sha16"]) if pm else
+                          "none: no PMC summary for these kernels (traffic / valu / valu_issue need "
+                          "tools/profile_round.sh on this kernel source)",
             "scene_device": scene_device(gpu.scene_info(h)),
+            "render_lanes": lanes,
+            "per_rank_ms_per_step": {"render_min": round(min(render_s) * 1e3, 3),
+                                     "render_max": round(max(render_s) * 1e3, 3),
+                                     "gather_and_resolve_max": round(max(gather_s) * 1e3, 3),
+                                     "note": "render = the rank's render call (its streams drained); then the "
+                                             "gather to rank 0 (N > 1) and rank 0's resolve_u8"},
             "samples_per_s": round(paths_all / elapsed, 1),
             "segments_per_path": round(segs_all / max(1.0, paths_all), 4),
             "ms_extend_per_step": round(ms_ext / a.steps, 3), "ms_shade_per_step": round(ms_shade / a.steps, 3),
@@ -439,14 +565,27 @@ def main():
         }
         out["cpu_baseline"] = None
         out["parity"] = None
-        if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"], ref = cpu_baseline(scene, nx, ny, spp, a.seed, a.cpu_baseline_seconds)
+        out["parity_frame"] = None
+        if not a.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle  # the checker and the CPU baseline only, after the timed region
+            host = host_cpu()
+            T = host["threads_used"]
+            o = oracle.build_scene(scene)
+            if world == 1:
+                out["cpu_baseline"], ref, per_row_pass = cpu_baseline(o, scene, nx, ny, spp, a.seed,
+                                                                      a.cpu_baseline_seconds, host)
+            else:                           # the CPU baseline is an N = 1 figure; the parity legs run at every N
+                ref, _, _, per_row_pass = oracle_band(o, scene, nx, ny, spp, a.seed, a.cpu_baseline_seconds, T)
             par = gpu_band_parity(scene, nx, ny, a.seed, ref, h, ctx)
             out["parity"] = par
             for k in ("rms_vs_oracle", "max_abs", "pixels_gt_1e-9"):
                 out[k] = par[k]
+            out["parity_frame"] = frame_rows_parity(o, last_frame, nx, ny, spp, a.seed, per_row_pass,
+                                                    a.cpu_baseline_seconds, T)
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

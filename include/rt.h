@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -54,12 +54,32 @@ int rt_device_count(int* out_count);
  * The render lanes' path pools belong to the context and are shared by every
  * scene rendered on it.  They are sized at the context's first render to
  * hold up to 288M paths, but at most 55 % of the device memory free at that
- * moment (RTAMD_MAX_PATHS overrides), and are kept for later renders;
+ * moment (RT_OPT_MAX_PATHS overrides), and are kept for later renders;
  * rt_context_release_pools frees them (the next render sizes them again),
  * e.g. before the caller allocates large buffers of its own. */
 int rt_context_create(int device, int* out_ctx);
 int rt_context_destroy(int ctx);
 int rt_context_release_pools(int ctx);
+
+/* Render-schedule options of a context (every scene rendered on it).  Value 0
+ * = the library's automatic choice (the default); negative values are refused.
+ * None of them changes an image: renders are bit-identical for any lane count,
+ * pool size and tail threshold (per-sample counter RNG, sample-ordered
+ * accumulation).
+ *   RT_OPT_LANES      render lanes (path pool + stream) kept in flight, 1..4;
+ *                     auto = 2, or 1 for scenes whose world BVH holds curves
+ *                     (the persistent curve kernel fills the chip by itself)
+ *   RT_OPT_MAX_PATHS  paths per pool (chunk of samples), >= 1024; auto = 288M,
+ *                     at most 55 % of free device memory for the lanes together
+ *                     (setting it makes the next render size the pools again)
+ *   RT_OPT_TAIL_PATHS a chunk with at most max(TAIL_PATHS, B / TAIL_DIV) live
+ *   RT_OPT_TAIL_DIV   paths (B = the chunk's camera samples) finishes in the
+ *                     persistent tail kernel; auto = 32768 and 256
+ *   RT_OPT_TAIL_OFF   nonzero: no tail kernel, every depth in the wavefront
+ *                     kernels (tests and A/B runs) */
+enum { RT_OPT_LANES = 1, RT_OPT_MAX_PATHS = 2, RT_OPT_TAIL_PATHS = 3, RT_OPT_TAIL_DIV = 4, RT_OPT_TAIL_OFF = 5 };
+int rt_context_set_option(int ctx, int option, int64_t value);
+int rt_context_get_option(int ctx, int option, int64_t* out_value);
 
 /* ---- scene building (replaces the closure-vector constructors) ---------- */
 int rt_scene_begin(int ctx, int* out_scene);

@@ -40,7 +40,7 @@ hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t
 hipError_t take_fault(uint32_t*);
 hipError_t take_curve_stats(unsigned long long out[2]);
 hipError_t launch_hit_rays(const DevScene&, const double*, uint32_t, double*, int32_t*, hipStream_t);
-hipError_t set_reject_cap(int);
+hipError_t set_test_caps(int, uint32_t);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -122,12 +122,19 @@ struct Lane {
 // A context owns the render lanes' path pools: every scene rendered on it
 // shares them (the C ABI renders one scene at a time per context), so a
 // second scene does not take a second 55 % of device memory.
+// The render schedule's knobs are options of the context (rt_context_set_option,
+// include/rt.h RT_OPT_*), 0 = the library's automatic choice.
 struct Context {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf accum_tmp, img_tmp;
     size_t pool_cap = 0;                       // paths per chunk (max_paths), fixed at the first render
     std::unique_ptr<Lane> lanes[kLanes];       // rt_context_release_pools frees them
+    int64_t opt_lanes = 0;                     // RT_OPT_LANES (0: 2, or 1 for curve-kernel scenes)
+    int64_t opt_max_paths = 0;                 // RT_OPT_MAX_PATHS (0: sized from free memory)
+    int64_t opt_tail_paths = 0;                // RT_OPT_TAIL_PATHS (0: 32768)
+    int64_t opt_tail_div = 0;                  // RT_OPT_TAIL_DIV (0: 256)
+    bool wavefront_only = false;               // RT_OPT_TAIL_OFF: no tail kernel (tests, A/B)
 };
 
 struct Scene {
@@ -1146,12 +1153,9 @@ std::string fault_text(uint32_t f) {
 // paths (22 chunks), 13 675 with 200M (12), 13 742 with 330M (8 chunks;
 // profiles/r02/pool/).  Default 288M paths, but at most what lets the render
 // lanes' pools (~272 B per path: two path-state pools, four hit queues, the
-// sample buffer) take 55 % of the device's free memory.  RTAMD_MAX_PATHS overrides.
-size_t max_paths(const int lanes) {
-    if (const char* e = std::getenv("RTAMD_MAX_PATHS")) {
-        const size_t v = (size_t)std::strtoull(e, nullptr, 10);
-        return v < 1024 ? 1024 : v;
-    }
+// sample buffer) take 55 % of the device's free memory.  RT_OPT_MAX_PATHS overrides.
+size_t max_paths(const Context& c, const int lanes) {
+    if (c.opt_max_paths > 0) return c.opt_max_paths < 1024 ? 1024 : (size_t)c.opt_max_paths;
     size_t v = (size_t)288 << 20;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
@@ -1163,29 +1167,27 @@ size_t max_paths(const int lanes) {
     return v < ((size_t)1 << 20) ? ((size_t)1 << 20) : v;
 }
 
-int lanes_wanted() {             // RTAMD_LANES: path pools kept in flight (1 = no overlap)
-    const char* e = std::getenv("RTAMD_LANES");
-    return e ? std::max(1, std::atoi(e)) : 2;
+int lanes_wanted(const Context& c) {   // RT_OPT_LANES: path pools kept in flight (1 = no overlap)
+    return c.opt_lanes > 0 ? (int)std::min<int64_t>(c.opt_lanes, kLanes) : 2;
 }
 // Scenes whose world BVH holds curves run the persistent curve kernel, whose
 // grid fills the chip by itself: a second lane's kernels only queue behind it
 // and its narrow tails, so one lane is faster (C5 at 64 spp: 200.3 vs 164.1
-// Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RTAMD_LANES overrides.
-int lanes_for(const DevScene& d) {
-    if (std::getenv("RTAMD_LANES")) return lanes_wanted();
+// Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RT_OPT_LANES overrides.
+int lanes_for(const Context& c, const DevScene& d) {
+    if (c.opt_lanes > 0) return lanes_wanted(c);
     const bool curve_kernel = d.n_bez > 0 && d.bvh_has_bez && d.n_med == 0 && d.n_klein == 0;
-    return curve_kernel ? 1 : lanes_wanted();
+    return curve_kernel ? 1 : lanes_wanted(c);
 }
 
-uint32_t tail_threshold() {
-    const char* e = std::getenv("RTAMD_TAIL_PATHS");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 32768u;
-}
-uint32_t tail_divisor() {
-    const char* e = std::getenv("RTAMD_TAIL_DIV");
+// A chunk's live paths at or below max(tail_threshold, B / tail_divisor) go to
+// the tail kernel; RT_OPT_TAIL_OFF keeps every depth in the wavefront.
+uint32_t tail_paths(const Context& c, const uint32_t B) {
+    if (c.wavefront_only) return 0u;
+    const uint32_t thr = c.opt_tail_paths > 0 ? (uint32_t)std::min<int64_t>(c.opt_tail_paths, 0xFFFFFFFFll) : 32768u;
     // B/256 with 288M-path pools (+0.9 % over B/128, profiles/r02/tail*/; B/128 was best with 96M pools)
-    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 256ul;
-    return v ? (uint32_t)v : 1u;
+    const uint32_t div = c.opt_tail_div > 0 ? (uint32_t)std::min<int64_t>(c.opt_tail_div, 0xFFFFFFFFll) : 256u;
+    return std::max<uint32_t>(thr, B / div);
 }
 
 constexpr size_t kStateBytesPerPath = sizeof(RayRec) + sizeof(PathRec) + sizeof(double) + sizeof(uint32_t);
@@ -1226,8 +1228,10 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         HIPCHK(take_fault(&stale));                  // a fault word left by another context's failed launch
         unsigned long long cs[2];
         HIPCHK(take_curve_stats(cs));                // counters start at zero for this render
-        const char* e = std::getenv("RTAMD_REJECT_CAP");  // tests: drive a sampler into its cap
-        HIPCHK(set_reject_cap(e ? std::max(0, std::atoi(e)) : 4096));
+        // tests: drive a sampler / the curve kernel's per-ray loop into its cap
+        const char* e = std::getenv("RTAMD_REJECT_CAP");
+        const char* rc = std::getenv("RTAMD_CURVE_RAY_CAP");
+        HIPCHK(set_test_caps(e ? std::max(0, std::atoi(e)) : 4096, rc ? (uint32_t)std::strtoul(rc, nullptr, 10) : 0u));
     }
     if (spp_count == 0) return 0;
 
@@ -1250,19 +1254,19 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // (680x381x1024 spp, the per-rank work at 8 GPUs) and 2.4 % at 1/4
     // (profiles/r02/mc/).
     // the cap is sized on the context's first render (before its pools exist), then kept
-    if (!c->pool_cap || std::getenv("RTAMD_MAX_PATHS")) c->pool_cap = max_paths(std::min(kLanes, lanes_wanted()));
+    if (!c->pool_cap) c->pool_cap = max_paths(*c, std::min(kLanes, lanes_wanted(*c)));
     const size_t cap_paths = c->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
     {
-        const int min_chunks = lanes_for(s->dev);   // one chunk per lane at least
+        const int min_chunks = lanes_for(*c, s->dev);   // one chunk per lane at least
         int n = (int)((spp_count + chunk - 1) / chunk);
         if (n < min_chunks) n = std::min(min_chunks, spp_count);
         if (n > 1 && (n & 1) && n < spp_count) ++n;
         chunk = (uint32_t)((spp_count + n - 1) / n);
     }
     const int nchunks = (int)((spp_count + chunk - 1) / chunk);
-    const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_for(s->dev)), nchunks));
+    const int nlanes = std::max(1, std::min(std::min(kLanes, lanes_for(*c, s->dev)), nchunks));
     const size_t cap = (size_t)npix * chunk;
     s->stats.chunks = (uint32_t)nchunks;
     s->stats.lanes = (uint32_t)nlanes;
@@ -1321,7 +1325,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // iteration (extend + shades + the survivor-count readback), or, below
     // the tail threshold, the tail kernel that finishes every remaining path.
     auto step = [&](Lane& L) -> int {
-        const uint32_t tail = std::max<uint32_t>(tail_threshold(), L.rp.B / tail_divisor());
+        const uint32_t tail = tail_paths(*c, L.rp.B);
         if (L.n == 0) { L.state = Lane::DONE; return 0; }
         if (L.depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
         if (L.n <= tail) {
@@ -1421,7 +1425,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         rp.B = npix * L.S;
         rp.compact = compact ? 1u : 0u;
         HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
-        const uint32_t tail = std::max<uint32_t>(tail_threshold(), rp.B / tail_divisor());
+        const uint32_t tail = tail_paths(*c, rp.B);
         L.fused_camera = s->cam_lds != 0 && rp.B > tail;     // the tail kernel starts from raygen's state
         if (!L.fused_camera) HIPCHK(launch_raygen(s->dev, rp, L.A, L.stream));
         L.cur = &L.A;
@@ -1557,6 +1561,45 @@ int rt_context_release_pools(int ctx) {
         if (L && L->stream) HIPCHK(hipStreamSynchronize(L->stream));
     for (auto& L : c->lanes) L.reset();
     c->pool_cap = 0;                               // the next render sizes them again
+    return 0;
+}
+
+int rt_context_set_option(int ctx, int option, int64_t value) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    if (value < 0) return fail("option value must be >= 0 (0 = automatic)");
+    switch (option) {
+    case RT_OPT_LANES:
+        if (value > kLanes) return fail("RT_OPT_LANES: at most " + std::to_string(kLanes) + " render lanes");
+        c->opt_lanes = value;
+        break;
+    case RT_OPT_MAX_PATHS:
+        if (value > ((int64_t)1 << 32)) return fail("RT_OPT_MAX_PATHS: at most 2^32 paths per pool");
+        c->opt_max_paths = value;
+        c->pool_cap = 0;                           // the next render sizes the pools again
+        break;
+    case RT_OPT_TAIL_PATHS: c->opt_tail_paths = value; break;
+    case RT_OPT_TAIL_DIV: c->opt_tail_div = value; break;
+    case RT_OPT_TAIL_OFF: c->wavefront_only = value != 0; break;
+    default: return fail("unknown context option " + std::to_string(option));
+    }
+    return 0;
+}
+
+int rt_context_get_option(int ctx, int option, int64_t* out) {
+    if (!out) return fail("null out pointer");
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    switch (option) {
+    case RT_OPT_LANES: *out = c->opt_lanes; break;
+    case RT_OPT_MAX_PATHS: *out = c->opt_max_paths; break;
+    case RT_OPT_TAIL_PATHS: *out = c->opt_tail_paths; break;
+    case RT_OPT_TAIL_DIV: *out = c->opt_tail_div; break;
+    case RT_OPT_TAIL_OFF: *out = c->wavefront_only ? 1 : 0; break;
+    default: return fail("unknown context option " + std::to_string(option));
+    }
     return 0;
 }
 

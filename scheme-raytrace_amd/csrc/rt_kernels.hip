@@ -44,9 +44,11 @@ namespace rtamd {
 __device__ unsigned int g_fault;
 __device__ __forceinline__ void raise_fault(const unsigned int bit) { atomicOr(&g_fault, bit); }
 constexpr int kRejectCap = 4096;               // rejection sampler attempts (P(reject) <= 0.48 per attempt)
-// the cap the samplers use: kRejectCap unless a test lowers it (RTAMD_REJECT_CAP, set_reject_cap) to
+// the cap the samplers use: kRejectCap unless a test lowers it (RTAMD_REJECT_CAP, set_test_caps) to
 // drive the fault path of a real sampler loop without a degenerate stream
 __device__ int g_reject_cap = kRejectCap;
+// k_extend_curves' per-ray iteration cap; 0 = the scene's bound (tests lower it: RTAMD_CURVE_RAY_CAP)
+__device__ uint32_t g_curve_ray_cap = 0;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;      // block_append / wave_append: the shard is full
 
 // ------------------------------------------------------------------ RNG
@@ -1680,8 +1682,11 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
     // a ray takes at most one step per node / leaf and one queue step per two curves: bound its
     // working iterations (a valid walk stays far below)
-    const uint32_t ray_cap = 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
+    const uint32_t ray_cap = g_curve_ray_cap ? g_curve_ray_cap : 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
     uint32_t ray_it = 0;
+    // a lane whose ray hit the cap stays out of the refill for good: candidates it queued may still sit
+    // in W.q / W.sv, and a new ray in the lane would take their results (W.done, hz / hkey)
+    bool dead = false;
 #ifdef RT_STATS
     uint32_t st_iter = 0, st_steps = 0, st_busy = 0, st_wait = 0, st_flush = 0;
     const unsigned long long st_clk0 = __builtin_amdgcn_s_memtime();
@@ -1691,7 +1696,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         // only iterations in which the lane itself works count: one waiting for a batch
         // other lanes trigger is bounded by their work (the last batch runs once no lane can add)
         if (active && (trav || pb < pe) && ++ray_it > ray_cap) {
-            raise_fault(RT_FAULT_PATH); active = false; trav = false; pb = pe;
+            raise_fault(RT_FAULT_PATH); active = false; trav = false; pb = pe; dead = true;
         }
 #ifdef RT_STATS
         ++st_iter;
@@ -1736,7 +1741,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
 #endif
         // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
-        const unsigned long long need = __ballot(!active);
+        const unsigned long long need = __ballot(!active && !dead);
         if (need && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
             const int leader = __ffsll((long long)need) - 1;
@@ -1744,7 +1749,7 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
             if ((int)lane == leader) base = atomicAdd(claim, cnt);
             base = (uint32_t)__shfl((int)base, leader, 64);
             if (base + cnt >= n) exhausted = true;
-            if (!active) {
+            if (!active && !dead) {
                 const uint32_t kk = base + lanes_below(need);
                 if (kk < n) {
                     k = kk;
@@ -2840,16 +2845,23 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
 #undef RT_FINISH
     return hipGetLastError();
 }
-// the samplers' attempt cap (render_impl: RTAMD_REJECT_CAP, tests only; default kRejectCap)
-hipError_t set_reject_cap(int cap) {
-    static int applied[64];                     // per device; 0 = not written yet (the default)
+// test hooks (render_impl: RTAMD_REJECT_CAP / RTAMD_CURVE_RAY_CAP, tests only): the samplers' attempt
+// cap (default kRejectCap) and the persistent curve kernel's per-ray iteration cap (0 = the scene's bound)
+hipError_t set_test_caps(int reject_cap, uint32_t curve_ray_cap) {
+    static int applied[64];                     // per device; 0 = not written yet (the defaults)
+    static uint32_t applied_ray[64];
     int dev = 0;
     HIP_RETURN_IF(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     const int have = applied[dev] ? applied[dev] - 1 : kRejectCap;
-    if (cap == have) return hipSuccess;
-    HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_reject_cap), &cap, sizeof cap));
-    applied[dev] = cap + 1;
+    if (reject_cap != have) {
+        HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_reject_cap), &reject_cap, sizeof reject_cap));
+        applied[dev] = reject_cap + 1;
+    }
+    if (curve_ray_cap != applied_ray[dev]) {
+        HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_curve_ray_cap), &curve_ray_cap, sizeof curve_ray_cap));
+        applied_ray[dev] = curve_ray_cap;
+    }
     return hipSuccess;
 }
 // the device fault word: read and clear (render_impl, after the render's streams are synchronised)

@@ -20,6 +20,8 @@ _c_u8_p = ctypes.POINTER(ctypes.c_uint8)
 RT_CAMERA_DOUBLES = 24
 RT_SKY_GRADIENT, RT_SKY_BLACK = 0, 1
 RT_RECT_XY, RT_RECT_XZ, RT_RECT_YZ = 0, 1, 2
+#: render-schedule options of a context (include/rt.h RT_OPT_*; 0 = automatic)
+RT_OPTIONS = {"lanes": 1, "max_paths": 2, "tail_paths": 3, "tail_div": 4, "tail_off": 5}
 
 
 class RtStats(ctypes.Structure):
@@ -60,6 +62,8 @@ _SIGNATURES = {
     "rt_context_create": [ctypes.c_int, _c_int_p],
     "rt_context_destroy": [ctypes.c_int],
     "rt_context_release_pools": [ctypes.c_int],
+    "rt_context_set_option": [ctypes.c_int, ctypes.c_int, ctypes.c_int64],
+    "rt_context_get_option": [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)],
     "rt_hit_rays": [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                     ctypes.POINTER(ctypes.c_int32)],
     "rt_scene_begin": [ctypes.c_int, _c_int_p],

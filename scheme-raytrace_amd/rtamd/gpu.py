@@ -1,5 +1,6 @@
 """Device side of the drop-in: contexts, scene upload and rendering through
 librtamd's C ABI.  There is no CPU fallback anywhere in this module."""
+import contextlib
 import ctypes
 
 import numpy as np
@@ -19,6 +20,33 @@ class Context:
         call("rt_context_create", int(device), ctypes.byref(h))
         self.handle = h.value
         self.device = device
+
+    def set_option(self, name, value):
+        """rt_context_set_option: a render-schedule option (_lib.RT_OPTIONS:
+        lanes, max_paths, tail_paths, tail_div, tail_off); 0 = automatic.
+        No option changes an image, only how the work is scheduled."""
+        call("rt_context_set_option", self.handle, _lib.RT_OPTIONS[name], int(value))
+
+    def get_option(self, name):
+        v = ctypes.c_int64(0)
+        call("rt_context_get_option", self.handle, _lib.RT_OPTIONS[name], ctypes.byref(v))
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **kv):
+        """Set options for the duration of a with-block, then restore them."""
+        old = {k: self.get_option(k) for k in kv}
+        try:
+            for k, val in kv.items():
+                self.set_option(k, val)
+            yield self
+        finally:
+            for k, val in old.items():
+                self.set_option(k, val)
+
+    def reset_options(self):
+        for k in _lib.RT_OPTIONS:
+            self.set_option(k, 0)
 
     def release_pools(self):
         """rt_context_release_pools: free the render lanes' path pools (the
@@ -253,6 +281,13 @@ def resolve_u8(accum, nx, ny, sample_count):
     call("rt_resolve_u8", a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), nx, ny, int(sample_count),
          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
     return out
+
+
+def resolve_u8_device(accum_ptr, nx, ny, sample_count, out_ptr, stream=None, ctx=None):
+    """rt_resolve_u8_device (main.scm:481-491) on device buffers: nx*ny*3 doubles -> bytes."""
+    ctx = ctx or default_context()
+    call("rt_resolve_u8_device", ctx.handle, ctypes.c_void_p(accum_ptr), nx, ny, int(sample_count),
+         ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or 0))
 
 
 def shard_pixels(nx, ny, shard, nshard):

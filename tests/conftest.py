@@ -41,3 +41,12 @@ def gpu_ctx():
     if gpu.device_count() < 1:
         pytest.fail("no HIP device visible for a gpu-marked test")
     return gpu.default_context(0)
+
+
+@pytest.fixture
+def sched(gpu_ctx):
+    """The default context with its render-schedule options (rt_context_set_option)
+    at their automatic values, restored after the test."""
+    gpu_ctx.reset_options()
+    yield gpu_ctx
+    gpu_ctx.reset_options()

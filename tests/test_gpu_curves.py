@@ -38,19 +38,19 @@ def _compare(a, b, n):
     return float(np.sqrt(np.mean(d ** 2))), float(d.max()), int((px > 1e-9).sum()), px.size
 
 
-def _env(monkeypatch, **kv):
+def _opts(ctx, **kv):
     for k, val in kv.items():
-        monkeypatch.setenv(k, str(val))
+        ctx.set_option(k, val)
 
 
-def test_c5_band_production_vs_oracle(gpu_ctx, oracle_mod, monkeypatch):
+def test_c5_band_production_vs_oracle(sched, oracle_mod):
     """C5 rows 524..555 (the middle of the frame, through the curve cloud),
     passes 252..255 of the 256-spp frame: 4 chunks of one pass (61 440 paths,
     above the tail threshold) on 2 lanes."""
     import torch
     nx, ny, y0, rows, s0, n = 1920, 1080, 524, 32, 252, 4
     sc = scenes.cornell_curves(nx, ny)
-    _env(monkeypatch, RTAMD_MAX_PATHS=rows * nx, RTAMD_LANES=2)
+    _opts(sched, max_paths=rows * nx, lanes=2)
     acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
     h = gpu.render_rows_device(sc, nx, ny, y0, rows, s0, n, SEED, acc.data_ptr())
     st = gpu.stats(h)
@@ -97,12 +97,12 @@ def _flat_curve_scene(nx, ny):
     return g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
 
 
-def test_flat_curves_in_pooled_batches_vs_oracle(gpu_ctx, oracle_mod, monkeypatch):
+def test_flat_curves_in_pooled_batches_vs_oracle(sched, oracle_mod):
     """Flat curves reach the pooled stage B of k_extend_curves (counted on the
     device), the render raises no fault, and the image matches the oracle."""
     nx, ny, spp = 128, 128, 64          # a flipped sample moves its pixel by ~1e-2 / spp
     sc = _flat_curve_scene(nx, ny)
-    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=1)
+    _opts(sched, tail_off=1, lanes=1)
     acc = np.zeros(nx * ny * 3)
     h = gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
     st = gpu.stats(h)
@@ -116,22 +116,20 @@ def test_flat_curves_in_pooled_batches_vs_oracle(gpu_ctx, oracle_mod, monkeypatc
     assert rms <= RMS_TOL
     assert nbad <= max(2, npx // 200)
     # the same render through the tail kernel's per-lane curve test: bit for bit
-    monkeypatch.delenv("RTAMD_TAIL_PATHS")
-    monkeypatch.delenv("RTAMD_TAIL_DIV")
-    monkeypatch.setenv("RTAMD_TAIL_PATHS", "100000000")
+    _opts(sched, tail_off=0, tail_paths=100000000)
     b = np.zeros(nx * ny * 3)
     gpu.render_host(sc, nx, ny, 0, spp, SEED, b)
     assert np.array_equal(acc, b)
 
 
 @pytest.mark.parametrize("wavefront", [False, True])
-def test_curve_deeper_than_walk_faults(gpu_ctx, monkeypatch, wavefront):
+def test_curve_deeper_than_walk_faults(sched, wavefront):
     """A curve of width 1e-13 spanning ~150 units needs ~27 subdivision levels
     (bezier.scm:180-193); the walk supports 24, so the render fails with the
     curve fault instead of a silently clamped image, and the next render of a
     normal scene is unaffected."""
     if wavefront:
-        _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000)
+        _opts(sched, tail_off=1)
     nx, ny, spp = 48, 48, 1
     white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
     curve = g.make_bezier(v.vec3(200, 200, 250), v.vec3(260, 380, 260), v.vec3(320, 150, 280), v.vec3(370, 330, 300),
@@ -146,7 +144,7 @@ def test_curve_deeper_than_walk_faults(gpu_ctx, monkeypatch, wavefront):
     assert np.isfinite(ok).all()
 
 
-def test_duplicate_curves_tie_to_the_later_curve(gpu_ctx, oracle_mod, monkeypatch):
+def test_duplicate_curves_tie_to_the_later_curve(sched, oracle_mod):
     """Curves duplicated exactly (same control points, other materials) in a
     BVH: every tie in z must go to the later curve of the list, as
     hit-obj-list's scan keeps a curve at z <= t-max (geometry.scm:41-46,
@@ -177,7 +175,7 @@ def test_duplicate_curves_tie_to_the_later_curve(gpu_ctx, oracle_mod, monkeypatc
         counts[em + 1] += 1
     print("duplicate curves: misses / floor-or-first / second / third copies hit:", counts)
     assert counts[2] > 0 and counts[3] > 0        # ties resolved to the later copies
-    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000)
+    _opts(sched, tail_off=1)
     acc = np.zeros(nx * ny * 3)
     gpu.render_host(sc, nx, ny, 0, 4, SEED, acc)
     ref, _ = o.render(nx, ny, 0, 4, SEED, nthreads=host_threads())
@@ -186,7 +184,7 @@ def test_duplicate_curves_tie_to_the_later_curve(gpu_ctx, oracle_mod, monkeypatc
     assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
 
 
-def test_few_curves_among_spheres_large_launch(gpu_ctx, oracle_mod, monkeypatch):
+def test_few_curves_among_spheres_large_launch(sched, oracle_mod, monkeypatch):
     """Two curves in the cover scene's world BVH (random-scene, main.scm:31-88,
     with its spheres), 960x540x16 spp in one chunk: 8.3M paths, thousands
     of rays per wave of the persistent curve kernel.  Candidates are rare, so a
@@ -205,7 +203,7 @@ def test_few_curves_among_spheres_large_launch(gpu_ctx, oracle_mod, monkeypatch)
                               0.15, gold))
     objs.append(g.make_bezier(v.vec3(-3, 2.0, 3), v.vec3(0, 0.5, -3), v.vec3(3, 3.0, 1), v.vec3(5, 0.8, 2), 0.1, red))
     sc = g.make_scene(objs, scenes.camera_for(nx, ny), g.sky_color)
-    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=1, RTAMD_MAX_PATHS=nx * ny * spp)
+    _opts(sched, tail_off=1, lanes=1, max_paths=nx * ny * spp)
     acc = np.zeros(nx * ny * 3)
     h = gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
     st = gpu.stats(h)
@@ -224,7 +222,7 @@ def test_few_curves_among_spheres_large_launch(gpu_ctx, oracle_mod, monkeypatch)
     assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
 
 
-def test_curve_walk_stack_overflow_bitwise(gpu_ctx, monkeypatch):
+def test_curve_walk_stack_overflow_bitwise(sched, monkeypatch):
     """The curve kernel's BVH4 walk pushes up to three children per node;
     commit_scene bounds its stack (rt_scene_info.curve_stack) and entries past
     the LDS column go to a per-lane overflow area in HBM, one region per render
@@ -232,7 +230,7 @@ def test_curve_walk_stack_overflow_bitwise(gpu_ctx, monkeypatch):
     deeper push takes that path, on two render lanes: the image must not
     change by a bit."""
     nx, ny, spp = 96, 64, 4
-    _env(monkeypatch, RTAMD_TAIL_PATHS=0, RTAMD_TAIL_DIV=1000000000, RTAMD_LANES=2, RTAMD_MAX_PATHS=nx * ny)
+    _opts(sched, tail_off=1, lanes=2, max_paths=nx * ny)
     base = np.zeros(nx * ny * 3)
     h = gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, base)
     info, st = gpu.scene_info(h), gpu.stats(h)
@@ -242,3 +240,28 @@ def test_curve_walk_stack_overflow_bitwise(gpu_ctx, monkeypatch):
     gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, low)
     print("curve walk stack: bound %d, LDS entries 1 vs %d" % (info["curve_stack"], info["tree_depth"]))
     assert np.array_equal(base, low)
+
+
+def test_curve_ray_cap_faults_without_hang(sched, monkeypatch):
+    """k_extend_curves bounds the iterations a lane works on one ray; a lane
+    that hits the bound raises the path fault and stays out of the refill, so
+    candidates it queued earlier can never be credited to a new ray (round-3
+    advice: a refilled lane then waited forever on W.done).  The cap is lowered
+    (RTAMD_CURVE_RAY_CAP, a device variable) so rays of a 16K-curve cloud hit
+    it mid-walk with candidates queued: the render must fail with the path
+    fault within the test's time limit, and the next render must be clean and
+    bit-identical to one before."""
+    nx, ny, spp = 96, 64, 2
+    _opts(sched, tail_off=1, lanes=1)
+    sc = scenes.cornell_curves(nx, ny, n_curves=1 << 14)
+    good = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, spp, SEED, good)
+    for cap in (3, 12):
+        monkeypatch.setenv("RTAMD_CURVE_RAY_CAP", str(cap))
+        acc = np.zeros(nx * ny * 3)
+        with pytest.raises(RtError, match="persistent kernel's path or ray"):
+            gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
+    monkeypatch.delenv("RTAMD_CURVE_RAY_CAP")
+    again = np.zeros(nx * ny * 3)
+    gpu.render_host(sc, nx, ny, 0, spp, SEED, again)
+    assert np.array_equal(good, again)

@@ -30,9 +30,6 @@ def _worker(rank, world, port, out_path, wavefront):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "scheme-raytrace_amd"))
-    if wavefront:                                # the wavefront kernels, not only the tail kernel
-        os.environ["RTAMD_TAIL_PATHS"] = "0"
-        os.environ["RTAMD_TAIL_DIV"] = "1000000000"
     import torch
     import torch.distributed as dist
 
@@ -45,6 +42,8 @@ def _worker(rank, world, port, out_path, wavefront):
     torch.cuda.set_device(0)
     scene = scenes.random_scene(NX, NY)
     ctx = gpu.default_context(0)
+    if wavefront:                                # the wavefront kernels, not only the tail kernel
+        ctx.set_option("tail_off", 1)
     local = torch.zeros(rdist.local_size(NX, NY, rank, world), dtype=torch.float64, device="cuda")
     frame = rdist.render_frame(scene, NX, NY, 0, SPP, SEED, rank, world, local=local, ctx=ctx)
     torch.cuda.synchronize()
@@ -57,14 +56,13 @@ def _worker(rank, world, port, out_path, wavefront):
 
 
 @pytest.mark.parametrize("world,wavefront", [(2, True), (3, False)])
-def test_multiprocess_tile_shards_equal_one_process_frame(gpu_ctx, tmp_path, monkeypatch, world, wavefront):
+def test_multiprocess_tile_shards_equal_one_process_frame(sched, tmp_path, monkeypatch, world, wavefront):
     import torch
     from rtamd import gpu, scenes
     out = str(tmp_path / "frame.npy")
     mp.spawn(_worker, args=(world, _free_port(), out, wavefront), nprocs=world, join=True)
     if wavefront:
-        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+        sched.set_option("tail_off", 1)
     full = torch.zeros(NX * NY * 3, dtype=torch.float64, device="cuda")
     gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
     torch.cuda.synchronize()
@@ -110,7 +108,7 @@ def _nccl_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_rccl_gather_world1_equals_render_device(gpu_ctx, tmp_path):
+def test_rccl_gather_world1_equals_render_device(sched, tmp_path):
     import torch
     from rtamd import gpu, scenes
     out = str(tmp_path / "frame.npy")
@@ -119,3 +117,32 @@ def test_rccl_gather_world1_equals_render_device(gpu_ctx, tmp_path):
     gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(np.load(out), full.cpu().numpy())
+
+
+def test_bench_two_ranks_self_verifying(tmp_path):
+    """bench.py at N=2 under torch.distributed.run (gloo rehearsal: both ranks
+    on cuda:0), launched as a fresh child process: the JSON line reports
+    n_gpus 2, per-rank timings, and both parity legs — a band re-rendered on
+    rank 0 and rows of the gathered frame itself — pass against the oracle.
+    This is the line the driver's 8-GPU SCALE run prints at every N."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RTAMD_DIST_BACKEND="gloo", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--spp", "8", "--nx", "320", "--ny", "180",
+           "--cpu-baseline-seconds", "2"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(json.dumps({k: d[k] for k in ("value", "n_gpus", "per_rank_ms_per_step")}),
+          d["parity"]["rms_vs_oracle"], d["parity_frame"]["rms_vs_oracle"], d["parity_frame"]["rows"])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"].startswith("tile-shard2")
+    assert d["cpu_baseline"] is None                        # an N = 1 figure only
+    assert d["parity"]["pass"] and d["parity_frame"]["pass"]
+    assert d["parity_frame"]["pixels_gt_1e-9"] <= max(2, d["parity_frame"]["pixels"] // 200)
+    assert d["per_rank_ms_per_step"]["render_max"] >= d["per_rank_ms_per_step"]["render_min"] > 0

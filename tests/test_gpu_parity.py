@@ -64,7 +64,7 @@ def test_scene_parity(name, nx, ny, spp, gpu_ctx, oracle_mod):
     assert nbad <= max(2, npx // 200)
 
 
-def test_full_width_band_parity(gpu_ctx, oracle_mod):
+def test_full_width_band_parity(sched, oracle_mod):
     """Config C2 geometry (1920x1080, aspect 16/9) on a band of rows."""
     nx, ny, spp = 1920, 1080, 2
     scene = scenes.random_scene(nx, ny)
@@ -82,23 +82,22 @@ def test_full_width_band_parity(gpu_ctx, oracle_mod):
     assert np.isfinite(acc).all() and (acc.reshape(-1, 3).sum(axis=1) > 0).mean() > 0.99
 
 
-def _schedule(monkeypatch, schedule):
+def _schedule(ctx, schedule):
     """"wavefront": the tail kernel off, so every depth runs through k_camera /
     k_extend_lds / k_shade with sharded compaction (these small renders would
     otherwise fit under the tail threshold and run in k_finish only)."""
     if schedule == "wavefront":
-        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+        sched.set_option("tail_off", 1)
 
 
 SCHEDULES = ["tail", "wavefront"]
 
 
 @pytest.mark.parametrize("schedule", SCHEDULES)
-def test_accumulate_across_calls_bitwise(gpu_ctx, monkeypatch, schedule):
+def test_accumulate_across_calls_bitwise(sched, monkeypatch, schedule):
     """spp passes in one call == the same passes split over calls (trace-all
     running sum, main.scm:480)."""
-    _schedule(monkeypatch, schedule)
+    _schedule(sched, schedule)
     nx, ny = 40, 30
     scene = scenes.random_scene(nx, ny)
     a = np.zeros(nx * ny * 3)
@@ -110,14 +109,14 @@ def test_accumulate_across_calls_bitwise(gpu_ctx, monkeypatch, schedule):
 
 
 @pytest.mark.parametrize("schedule", SCHEDULES)
-def test_batching_independent_bitwise(gpu_ctx, monkeypatch, schedule):
+def test_batching_independent_bitwise(sched, monkeypatch, schedule):
     """Results do not depend on the path-pool size (chunking of samples)."""
-    _schedule(monkeypatch, schedule)
+    _schedule(sched, schedule)
     nx, ny = 50, 20
     scene = scenes.cornell_box(nx, ny)
     a = np.zeros(nx * ny * 3)
     gpu.render_host(scene, nx, ny, 0, 8, SEED, a)
-    monkeypatch.setenv("RTAMD_MAX_PATHS", "1024")
+    sched.set_option("max_paths", 1024)
     b = np.zeros(nx * ny * 3)
     gpu.render_host(scene, nx, ny, 0, 8, SEED, b)
     assert np.array_equal(a, b)
@@ -125,27 +124,27 @@ def test_batching_independent_bitwise(gpu_ctx, monkeypatch, schedule):
 
 @pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("lanes", ["1", "2"])
-def test_lanes_and_chunks_bitwise(gpu_ctx, monkeypatch, lanes, schedule):
+def test_lanes_and_chunks_bitwise(sched, monkeypatch, lanes, schedule):
     """Overlapped path pools (lanes) and many small chunks give the one-chunk
     image bit for bit: chunks are accumulated in sample order whichever lane
     finishes first."""
-    _schedule(monkeypatch, schedule)
+    _schedule(sched, schedule)
     nx, ny, spp = 48, 40, 12
     scene = scenes.random_scene(nx, ny)
     a = np.zeros(nx * ny * 3)
     gpu.render_host(scene, nx, ny, 0, spp, SEED, a)
-    monkeypatch.setenv("RTAMD_MAX_PATHS", str(nx * ny * 2))   # 6 chunks of 2 spp
-    monkeypatch.setenv("RTAMD_LANES", lanes)
+    sched.set_option("max_paths", nx * ny * 2)   # 6 chunks of 2 spp
+    sched.set_option("lanes", int(lanes))
     b = np.zeros(nx * ny * 3)
     gpu.render_host(scene, nx, ny, 0, spp, SEED, b)
     assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("schedule", SCHEDULES)
-def test_shards_union_bitwise(gpu_ctx, monkeypatch, schedule):
+def test_shards_union_bitwise(sched, monkeypatch, schedule):
     """Interleaved tile shards (the multi-GPU partition) reassemble the
     single-device image bit for bit."""
-    _schedule(monkeypatch, schedule)
+    _schedule(sched, schedule)
     import torch
     nx, ny, spp = 70, 45, 3
     scene = scenes.random_scene(nx, ny)
@@ -158,7 +157,7 @@ def test_shards_union_bitwise(gpu_ctx, monkeypatch, schedule):
     assert torch.equal(full, parts)
 
 
-def test_trace_all_passes_match_oracle_image(gpu_ctx, oracle_mod):
+def test_trace_all_passes_match_oracle_image(sched, oracle_mod):
     """Renderer.trace_all pass by pass (main.scm:471-491) and the u8 image."""
     from rtamd.render import Renderer
     nx, ny = 32, 24
@@ -173,7 +172,7 @@ def test_trace_all_passes_match_oracle_image(gpu_ctx, oracle_mod):
     assert diff.max() <= 1 and (diff > 0).sum() <= 2
 
 
-def test_edge_sizes(gpu_ctx, oracle_mod):
+def test_edge_sizes(sched, oracle_mod):
     for nx, ny in ((1, 1), (17, 3), (3, 17)):
         scene = scenes.test_scene(nx, ny)
         acc, ref = _both(scene, nx, ny, 2, oracle_mod)
@@ -181,7 +180,7 @@ def test_edge_sizes(gpu_ctx, oracle_mod):
         assert rms <= RMS_TOL
 
 
-def test_zero_spp_is_noop(gpu_ctx):
+def test_zero_spp_is_noop(sched):
     nx, ny = 8, 8
     scene = scenes.test_scene(nx, ny)
     a = np.full(nx * ny * 3, 0.25)
@@ -189,7 +188,7 @@ def test_zero_spp_is_noop(gpu_ctx):
     assert (a == 0.25).all()
 
 
-def test_errors_are_loud(gpu_ctx):
+def test_errors_are_loud(sched):
     from rtamd._lib import RtError, call
     with pytest.raises(RtError):
         call("rt_render", 987654, 4, 4, 0, 1, ctypes.c_uint64(1), None)
@@ -204,7 +203,7 @@ def test_errors_are_loud(gpu_ctx):
             ctypes.POINTER(ctypes.c_double)))
 
 
-def test_device_resolve_matches_host(gpu_ctx):
+def test_device_resolve_matches_host(sched):
     import torch
     nx, ny = 33, 21
     scene = scenes.random_scene(nx, ny)
@@ -218,7 +217,7 @@ def test_device_resolve_matches_host(gpu_ctx):
     assert np.array_equal(out.cpu().numpy(), host)
 
 
-def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
+def test_bvh_matches_flat_list_bitwise(sched, monkeypatch):
     """The BVH only culls: the image equals the brute-force flat list
     (geometry.scm:33-50) bit for bit."""
     nx, ny, spp = 64, 40, 4
@@ -234,14 +233,13 @@ def test_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("wavefront", [False, True])
-def test_sah_builders_same_image_bitwise(gpu_ctx, monkeypatch, wavefront):
+def test_sah_builders_same_image_bitwise(sched, monkeypatch, wavefront):
     """The exact-sweep SAH tree (default for sphere trees) and the binned
     one (RTAMD_BVH_SWEEP=0) only cull differently: same image, bit for bit,
     through the tail kernel and through the wavefront kernels."""
     nx, ny, spp = 64, 40, 4
     if wavefront:
-        monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-        monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+        sched.set_option("tail_off", 1)
     imgs = []
     for sweep in ("0", None):
         if sweep is None:
@@ -305,7 +303,7 @@ def _many_spheres_scene(nx, ny):
 
 
 @pytest.mark.parametrize("make", [_static_cover_scene, _many_spheres_scene])
-def test_kernel_paths_match_flat_list_bitwise(gpu_ctx, monkeypatch, make):
+def test_kernel_paths_match_flat_list_bitwise(sched, monkeypatch, make):
     """Scenes that take the other closest-hit paths (time-0 tree for camera
     rays; trees too big for LDS) equal the brute-force flat list bit for bit."""
     nx, ny, spp = 48, 27, 4
@@ -321,7 +319,7 @@ def test_kernel_paths_match_flat_list_bitwise(gpu_ctx, monkeypatch, make):
 
 
 @pytest.mark.parametrize("make", [scenes.random_scene, _moving_mix_scene])
-def test_time0_bvh_matches_all_times_bvh_bitwise(gpu_ctx, monkeypatch, make):
+def test_time0_bvh_matches_all_times_bvh_bitwise(sched, monkeypatch, make):
     """Scattered rays (time 0) traverse the time-0 tree with moving spheres
     frozen at center(0); the image equals the one from the all-times tree and
     the flat list bit for bit."""
@@ -360,7 +358,7 @@ def test_gpu_vs_reference_fixtures(name, gpu_ctx):
     assert (np.abs(img.astype(int) - np.array(g["image"])) <= 1).all()
 
 
-def test_curve_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
+def test_curve_bvh_matches_flat_list_bitwise(sched, monkeypatch):
     """Curves in the BVH (boxes = control points +- width/2, t range widened
     for |dir| < 1 rays, Q10) give the flat list's image bit for bit."""
     nx, ny, spp = 64, 36, 2
@@ -373,7 +371,7 @@ def test_curve_bvh_matches_flat_list_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(a, b)
 
 
-def test_media_in_list_order(gpu_ctx, oracle_mod):
+def test_media_in_list_order(sched, oracle_mod):
     """A medium listed between other objects (and a sphere-bounded one, and
     one under an instance) draws its random number with the closest hit of
     the objects before it only: GPU vs oracle."""
@@ -399,7 +397,7 @@ def test_media_in_list_order(gpu_ctx, oracle_mod):
     assert nbad <= max(2, npx // 200)
 
 
-def test_sphere_light_mixture(gpu_ctx, oracle_mod):
+def test_sphere_light_mixture(sched, oracle_mod):
     """pdf.scm mixture toward a sphere light (extension f2): GPU vs oracle."""
     from rtamd import scene as g
     from rtamd.camera import make_camera
@@ -416,7 +414,7 @@ def test_sphere_light_mixture(gpu_ctx, oracle_mod):
     assert nbad <= max(2, npx // 200)
 
 
-def test_c_example_matches_python_host(gpu_ctx, tmp_path):
+def test_c_example_matches_python_host(sched, tmp_path):
     """The C-ABI example (examples/cornell.c) and the Python host render the
     same cornell-box to the same PPM bytes."""
     import subprocess
@@ -440,7 +438,7 @@ _WAVEFRONT_SCENES = ["cover", "cover_marble", "test_scene2", "cornell", "cornell
 
 
 @pytest.mark.parametrize("name", _WAVEFRONT_SCENES)
-def test_wavefront_matches_tail_kernel_bitwise(gpu_ctx, monkeypatch, name):
+def test_wavefront_matches_tail_kernel_bitwise(sched, monkeypatch, name):
     """Small renders run entirely in the tail kernel (k_finish: extend + shade
     per lane).  With the tail switched off the same render goes through the
     wavefront kernels (k_camera / raygen, k_extend_lds / k_extend<F> /
@@ -450,12 +448,10 @@ def test_wavefront_matches_tail_kernel_bitwise(gpu_ctx, monkeypatch, name):
     nx, ny, spp = 40, 24, 3
     if name.startswith("curves") or "bezier" in name:
         nx, ny, spp = 32, 18, 2
-    monkeypatch.delenv("RTAMD_TAIL_PATHS", raising=False)
-    monkeypatch.delenv("RTAMD_TAIL_DIV", raising=False)
+    sched.set_option("tail_off", 0)
     a = np.zeros(nx * ny * 3)
     gpu.render_host(scenes.SCENES[name](nx, ny), nx, ny, 0, spp, SEED, a)
-    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    sched.set_option("tail_off", 1)
     b = np.zeros(nx * ny * 3)
     gpu.render_host(scenes.SCENES[name](nx, ny), nx, ny, 0, spp, SEED, b)
     assert np.isfinite(a).all()
@@ -463,7 +459,7 @@ def test_wavefront_matches_tail_kernel_bitwise(gpu_ctx, monkeypatch, name):
 
 
 @pytest.mark.parametrize("flat_curves", [False, True])
-def test_curve_kernels_bitwise(gpu_ctx, monkeypatch, flat_curves):
+def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     """Curves, spheres and moving spheres in one world BVH between rect
     groups, through the wavefront: the persistent curve kernel, the per-ray
     curve kernel and the flat list give the same image bit for bit.
@@ -503,8 +499,7 @@ def test_curve_kernels_bitwise(gpu_ctx, monkeypatch, flat_curves):
              g.make_yz_rect(0, 555, 0, 555, 0, red),
              g.flip_normals(g.make_xy_rect(0, 555, 0, 555, 555, white))]
     sc = g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
-    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+    sched.set_option("tail_off", 1)
     imgs = []
     for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {}, {"RTAMD_CURVE_BLOCKS": "3"}):
         for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS"):
@@ -521,7 +516,7 @@ def test_curve_kernels_bitwise(gpu_ctx, monkeypatch, flat_curves):
 
 @pytest.mark.parametrize("name", ["cover", "cornell", "test_bezier", "cornell_bezier", "curves_small", "cornell_klein",
                                   "bvh_sah"])
-def test_hit_rays_vs_oracle_hit_world(gpu_ctx, oracle_mod, name):
+def test_hit_rays_vs_oracle_hit_world(sched, oracle_mod, name):
     """rt_hit_rays (the extend kernels' closest_hit on a caller's rays) against
     the oracle's hit-obj-list over the same scene list (orc_hit_world): camera
     and scattered-like rays, unit and raw directions, |dir| < 1, times 0 and
@@ -560,6 +555,6 @@ def test_hit_rays_vs_oracle_hit_world(gpu_ctx, oracle_mod, name):
     assert len(bad) <= n // 1000, bad[:5]
 
 
-def test_hit_rays_refuses_media(gpu_ctx):
+def test_hit_rays_refuses_media(sched):
     with pytest.raises(RtError, match="media"):
         gpu.hit_rays(scenes.cornell_smoke(16, 16), np.zeros((1, 7)))

@@ -22,9 +22,8 @@ RMS_TOL = 1e-4
 SEED = 0x5EED0002
 
 
-def _wavefront_only(monkeypatch):
-    monkeypatch.setenv("RTAMD_TAIL_PATHS", "0")
-    monkeypatch.setenv("RTAMD_TAIL_DIV", "1000000000")
+def _wavefront_only(ctx):
+    ctx.set_option("tail_off", 1)
 
 
 def _compare(a, b, n):
@@ -42,20 +41,11 @@ def c2_band(gpu_ctx, oracle_mod):
     import torch
     nx, ny, y0, rows, s0, n = 1920, 1080, 400, 16, 1000, 24
     scene = scenes.random_scene(nx, ny)
-    old = {k: os.environ.get(k) for k in ("RTAMD_MAX_PATHS", "RTAMD_LANES")}
-    os.environ["RTAMD_MAX_PATHS"] = str(3 * rows * nx)
-    os.environ["RTAMD_LANES"] = "2"
-    try:
+    with gpu_ctx.options(max_paths=3 * rows * nx, lanes=2):
         acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
         h = gpu.render_rows_device(scene, nx, ny, y0, rows, s0, n, SEED, acc.data_ptr())
         st = gpu.stats(h)
         got = acc.cpu().numpy()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
     ref = np.zeros(nx * ny * 3)
     lo, hi = y0 * nx, (y0 + rows) * nx
     oracle_mod.build_scene(scene).render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=host_threads())
@@ -78,19 +68,60 @@ def test_production_band_vs_oracle(c2_band):
     assert not b["got"][:3 * lo].any() and not b["got"][3 * hi:].any()
 
 
-def test_production_band_wavefront_to_depth_cap_bitwise(c2_band, monkeypatch):
+def test_production_band_wavefront_to_depth_cap_bitwise(c2_band, sched):
     """The same band with the tail kernel off (every depth in the wavefront,
     one lane, other chunking): bit for bit the production result."""
     import torch
     b = c2_band
-    _wavefront_only(monkeypatch)
-    monkeypatch.setenv("RTAMD_LANES", "1")
-    monkeypatch.setenv("RTAMD_MAX_PATHS", str(5 * b["rows"] * b["nx"]))
+    _wavefront_only(sched)
+    sched.set_option("lanes", 1)
+    sched.set_option("max_paths", 5 * b["rows"] * b["nx"])
     acc = torch.zeros(b["nx"] * b["ny"] * 3, dtype=torch.float64, device="cuda")
     h = gpu.render_rows_device(b["scene"], b["nx"], b["ny"], b["y0"], b["rows"], b["s0"], b["n"], SEED,
                                acc.data_ptr())
     assert gpu.stats(h).finish_paths == 0
     assert np.array_equal(acc.cpu().numpy(), b["got"])
+
+
+# Configs C3 / C4 (and C4 with the f2 mixture) at their stated frame sizes, on
+# a band at the top sample indices of their frames, through the production
+# schedule: chunks of `chunk` passes (above the tail threshold) on two render
+# lanes, so k_camera / k_extend_lds (or k_extend<F>) and the per-material
+# k_shade queues do the wide iterations and k_finish only the tail.
+#   name: (nx, ny, y0, rows, first pass, passes, passes per chunk)
+BANDS = {
+    "cover_marble": (1920, 1080, 400, 16, 1000, 24, 3),       # C3: marble ground (Perlin tables in LDS)
+    "cornell": (1024, 1024, 480, 64, 4088, 8, 2),             # C4: cornell-box, 4096-spp frame
+    "cornell_mixture": (1024, 1024, 480, 64, 4088, 8, 2),     # C4 + f2 light / cosine mixture
+}
+
+
+@pytest.mark.parametrize("name", sorted(BANDS))
+def test_config_band_production_vs_oracle(sched, oracle_mod, name):
+    import torch
+    nx, ny, y0, rows, s0, n, per_chunk = BANDS[name]
+    scene = scenes.SCENES[name](nx, ny)
+    sched.set_option("max_paths", per_chunk * rows * nx)
+    sched.set_option("lanes", 2)
+    acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    h = gpu.render_rows_device(scene, nx, ny, y0, rows, s0, n, SEED, acc.data_ptr())
+    st = gpu.stats(h)
+    got = acc.cpu().numpy()
+    ref = np.zeros(nx * ny * 3)
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    _, segs = oracle_mod.build_scene(scene).render(nx, ny, s0, n, SEED, ref, lo, hi, nthreads=host_threads())
+    rms, dmax, nbad, npx = _compare(got[3 * lo:3 * hi], ref[3 * lo:3 * hi], n)
+    print("%s band rows %d..%d passes %d..%d: rms=%.3e max=%.3e pixels>1e-9: %d/%d segments gpu %d oracle %d "
+          "(wavefront %d, tail paths %d of %d) chunks=%d lanes=%d"
+          % (name, y0, y0 + rows - 1, s0, s0 + n - 1, rms, dmax, nbad, npx, st.segments, segs, st.extend_rays,
+             st.finish_paths, st.paths, st.chunks, st.lanes))
+    assert st.chunks >= 4 and st.lanes == 2, (st.chunks, st.lanes)
+    # the wavefront kernels traced every camera ray and the wide scattered iterations; the tail kernel only
+    # took each chunk's last few paths
+    assert st.extend_rays > st.paths and st.finish_paths < st.paths
+    assert rms <= RMS_TOL
+    assert nbad <= max(2, npx // 200)
+    assert not got[:3 * lo].any() and not got[3 * hi:].any()
 
 
 def test_trace_line_row_by_row_equals_trace_all(gpu_ctx):
@@ -117,10 +148,10 @@ def test_trace_line_row_by_row_equals_trace_all(gpu_ctx):
     assert c.anim_sample_count == 3 and c.current_y == 0
 
 
-def test_rows_match_frame_bitwise(gpu_ctx, monkeypatch):
+def test_rows_match_frame_bitwise(sched):
     """Row bands (rt_render_rows) through the wavefront reassemble the
     full-frame render bit for bit."""
-    _wavefront_only(monkeypatch)
+    _wavefront_only(sched)
     nx, ny, spp = 64, 36, 4
     scene = scenes.random_scene(nx, ny)
     full = np.zeros(nx * ny * 3)
@@ -131,12 +162,12 @@ def test_rows_match_frame_bitwise(gpu_ctx, monkeypatch):
     assert np.array_equal(full, parts)
 
 
-def test_compact_shards_match_frame(gpu_ctx, monkeypatch):
+def test_compact_shards_match_frame(sched):
     """rt_render_shard_device (a rank's compact accumulator, as bench.py's
     multi-GPU path uses) scattered by rt_shard_pixels equals the frame."""
     import torch
     from rtamd import dist as rdist
-    _wavefront_only(monkeypatch)
+    _wavefront_only(sched)
     nx, ny, spp, world = 70, 45, 3, 3
     scene = scenes.random_scene(nx, ny)
     full = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
@@ -190,10 +221,10 @@ def _noise_scene(nx, ny):
 
 
 @pytest.mark.parametrize("wavefront", [False, True])
-def test_noise_texture_vs_oracle(gpu_ctx, oracle_mod, monkeypatch, wavefront):
+def test_noise_texture_vs_oracle(sched, oracle_mod, wavefront):
     nx, ny, spp = 64, 36, 8
     if wavefront:
-        _wavefront_only(monkeypatch)
+        _wavefront_only(sched)
     sc = _noise_scene(nx, ny)
     acc = np.zeros(nx * ny * 3)
     gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
@@ -206,7 +237,7 @@ def test_noise_texture_vs_oracle(gpu_ctx, oracle_mod, monkeypatch, wavefront):
 
 
 @pytest.mark.parametrize("wavefront", [False, True])
-def test_sampler_cap_raises_fault_not_hang(gpu_ctx, monkeypatch, wavefront):
+def test_sampler_cap_raises_fault_not_hang(sched, monkeypatch, wavefront):
     """Every device loop that waits on random data has an attempt cap a valid
     stream cannot reach (rt_kernels.hip kRejectCap = 4096, P(reject) <= 0.48).
     RTAMD_REJECT_CAP=0 lowers the cap so the real samplers — random-in-unit-disk
@@ -218,7 +249,7 @@ def test_sampler_cap_raises_fault_not_hang(gpu_ctx, monkeypatch, wavefront):
     from rtamd._lib import RtError
     nx, ny, spp = 96, 54, 8
     if wavefront:
-        _wavefront_only(monkeypatch)
+        _wavefront_only(sched)
     scene = scenes.random_scene(nx, ny)
     good = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
     gpu.render_device(scene, nx, ny, 0, spp, SEED, good.data_ptr())
@@ -259,14 +290,14 @@ def test_pools_shared_per_context_and_released(gpu_ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["RTAMD_NO_EXTEND_LDS", "RTAMD_NO_CAMERA_LDS", "RTAMD_FINISH_GENERIC", "RTAMD_NO_SOLO"])
-def test_kernel_variants_bitwise(gpu_ctx, monkeypatch, switch):
+def test_kernel_variants_bitwise(sched, monkeypatch, switch):
     """The cover scene's specialised kernels (k_extend_lds, k_camera, the SOLO
     tail, the SOLO direct-leaf walk) against the general ones (k_extend<F>,
     k_raygen + k_extend, the group-loop tail, leaf records): the same image
     bit for bit."""
     nx, ny, spp = 64, 36, 3
     if switch != "RTAMD_FINISH_GENERIC":
-        _wavefront_only(monkeypatch)
+        _wavefront_only(sched)
     a = np.zeros(nx * ny * 3)
     gpu.render_host(scenes.random_scene(nx, ny), nx, ny, 0, spp, SEED, a)
     monkeypatch.setenv(switch, "1")

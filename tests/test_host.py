@@ -35,10 +35,15 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_errors_without_gpu():
     L = _lib.lib()
-    assert L.rt_abi_version() == 4
+    assert L.rt_abi_version() == 5
     h = ctypes.c_int(0)
     assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
     assert b"invalid context" in L.rt_last_error()
+    # render-schedule options are per context: an unknown handle is refused before any device call
+    assert L.rt_context_set_option(424242, 1, 2) != 0
+    assert b"invalid context" in L.rt_last_error()
+    v = ctypes.c_int64(7)
+    assert L.rt_context_get_option(424242, 1, ctypes.byref(v)) != 0 and v.value == 7
     with pytest.raises(_lib.RtError):
         _lib.call("rt_shard_pixels", 4, 4, 5, 2, None, ctypes.byref(ctypes.c_int64()))
 
@@ -187,7 +192,7 @@ def test_c_example_builds_against_the_abi(tmp_path):
     import subprocess
     exe = _build_c_example(tmp_path)
     out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
-    assert out.strip() == "rt_abi_version 4"
+    assert out.strip() == "rt_abi_version 5"
 
 
 def test_load_points_and_points_to_bezier(tmp_path):

@@ -26,15 +26,15 @@ def main():
     p.add_argument("--ny", type=int, default=1080)
     p.add_argument("--spp", type=int, default=256)
     p.add_argument("--rounds", type=int, default=3)
-    p.add_argument("--lanes", default=None, help="RTAMD_LANES for every variant")
+    p.add_argument("--lanes", default=None, help="render lanes (RT_OPT_LANES) for every variant")
     p.add_argument("variants", nargs="+", help="name:ENV=V,ENV2=V2 (name: alone = defaults)")
     a = p.parse_args()
     import torch
     from rtamd import gpu, scenes
     from rtamd._lib import call
-    if a.lanes:
-        os.environ["RTAMD_LANES"] = a.lanes
     ctx = gpu.default_context(0)
+    if a.lanes:
+        ctx.set_option("lanes", int(a.lanes))
     vs = []
     for spec in a.variants:
         name, _, envs = spec.partition(":")

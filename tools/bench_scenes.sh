@@ -15,5 +15,5 @@ for s in $SC; do
     *) A="--steps 1 --warmup 1" ;;
   esac
   timeout -k 10 900 python -u bench.py --scene $s $A > $O/bench_$s.log 2>&1 || { echo "bench $s failed"; tail -20 $O/bench_$s.log; exit 1; }
-  grep '^{' $O/bench_$s.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); p=d.get('parity') or {}; print(d['config']['workload'], d['value'], d['ms_per_step'], p.get('rms_vs_oracle'), p.get('pixels_gt_1e-9'), (d.get('roofline_isolated') or {}).get('frac'))"
+  grep '^{' $O/bench_$s.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); p=d.get('parity') or {}; print(d['config']['workload'], d['value'], d['ms_per_step'], p.get('rms_vs_oracle'), p.get('pixels_gt_1e-9'), (d.get('roofline') or {}).get('frac'), (d.get('roofline_frame') or {}).get('frac'), (d.get('parity_frame') or {}).get('rms_vs_oracle'), (d.get('parity_frame') or {}).get('pixels_gt_1e-9'))"
 done

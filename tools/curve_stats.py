@@ -3,7 +3,7 @@
 its wave cycles and how busy stage B's lanes are.
 
 Build:  make -C scheme-raytrace_amd/csrc EXTRA=-DRT_STATS OUT=../rtamd/librtamd_stats.so
-Run:    RTAMD_LIB=scheme-raytrace_amd/rtamd/librtamd_stats.so RTAMD_LANES=1 python3 tools/curve_stats.py [spp]
+Run:    RTAMD_LIB=scheme-raytrace_amd/rtamd/librtamd_stats.so python3 tools/curve_stats.py [spp]
 """
 import ctypes
 import json
@@ -21,8 +21,9 @@ def main():
     nx, ny = 1920, 1080
     lib = ctypes.CDLL(_lib.LIB_PATH)
     b = (ctypes.c_ulonglong * 48)()
-    os.environ.setdefault("RTAMD_TAIL_PATHS", "0")
-    os.environ.setdefault("RTAMD_TAIL_DIV", "1000000000")
+    ctx = gpu.default_context(0)
+    ctx.set_option("lanes", 1)
+    ctx.set_option("tail_off", 1)              # the wavefront curve kernel at every depth
     sc = scenes.cornell_curves(nx, ny)
     acc = np.zeros(nx * ny * 3)
     gpu.render_host(sc, nx, ny, 0, 1, 0x5EED0002, acc)          # upload + warm

@@ -7,12 +7,15 @@ from rtamd import gpu
 from test_gpu_curves import _flat_curve_scene
 nx = ny = 128
 out = {}
-for name, env in [("tail", {"RTAMD_TAIL_PATHS": "100000000"}),
-                  ("wave", {"RTAMD_TAIL_PATHS": "0", "RTAMD_TAIL_DIV": "1000000000"}),
-                  ("flatlist", {"RTAMD_TAIL_PATHS": "100000000", "RTAMD_BVH_MIN": "1000000000"})]:
-    for k in ("RTAMD_TAIL_PATHS", "RTAMD_TAIL_DIV", "RTAMD_BVH_MIN"):
-        os.environ.pop(k, None)
+ctx = gpu.default_context(0)
+for name, opts, env in [("tail", {"tail_paths": 100000000}, {}),
+                        ("wave", {"tail_off": 1}, {}),
+                        ("flatlist", {"tail_paths": 100000000}, {"RTAMD_BVH_MIN": "1000000000"})]:
+    os.environ.pop("RTAMD_BVH_MIN", None)
     os.environ.update(env)
+    ctx.reset_options()
+    for k, val in opts.items():
+        ctx.set_option(k, val)
     sc = _flat_curve_scene(nx, ny)
     for s in range(4):
         a = np.zeros(nx * ny * 3)

@@ -11,4 +11,4 @@ tail -3 $O/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; cat $O/smoke.log; exit 1; }
 cat $O/smoke.log
 timeout -k 10 400 python -u bench.py > $O/bench_c2.log 2>&1 || { echo "bench failed"; tail -30 $O/bench_c2.log; exit 1; }
-grep '^{' $O/bench_c2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('rms_vs_oracle'), d.get('max_abs'), d.get('pixels_gt_1e-9'), d['roofline_isolated']['frac'], d['cpu_baseline']['value'], d['cpu_baseline']['cores'])"
+grep '^{' $O/bench_c2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('rms_vs_oracle'), d.get('max_abs'), d.get('pixels_gt_1e-9'), d['roofline']['frac'], (d.get('roofline_frame') or {}).get('frac'), (d.get('parity_frame') or {}).get('rms_vs_oracle'), d['cpu_baseline']['value'], d['cpu_baseline']['cores'])"

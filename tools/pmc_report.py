@@ -24,6 +24,7 @@ which bench.py reads for roofline.traffic and the valu / valu_issue objects.
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -157,6 +158,11 @@ def main():
               "note": "one frame at the bench configuration; FETCH_SIZE doubled (16-B record loads)"}
     report["extend_phase"] = pmc_ext
     report["shade_phase"] = pmc_sh
+    # stamp: bench.py uses these counters only while the kernels are the ones they were measured on
+    with open(os.path.join(ROOT, "scheme-raytrace_amd", "csrc", "rt_kernels.hip"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    for rec in (report, pmc_ext, pmc_sh):
+        rec["kernel_sha16"] = sha
     json.dump(report, open(out_path, "w"), indent=1)
     json.dump(pmc_ext, open(os.path.join(ROOT, "profiles", "pmc_extend.json"), "w"), indent=1)
     json.dump(pmc_sh, open(os.path.join(ROOT, "profiles", "pmc_shade.json"), "w"), indent=1)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One round's profile set at the BENCH configuration (C2: cover scene, 1920x1080x1024 spp, one frame),
 # run on the GPU box from the repo root:
-#   1. rocprofv3 kernel trace + stats, two render lanes (the timed bench) and one lane (roofline_isolated)
+#   1. rocprofv3 kernel trace + stats, two render lanes (the timed bench) and one lane (bench.py's roofline)
 #   2. PMC passes over every kernel of one frame (each pass a run of its own, within the per-block limits):
 #        fetch: FETCH_SIZE    write: WRITE_SIZE
 #        sq1:   VALUBusy VALUUtilization LdsUtil LdsBankConflict OccupancyPercent + SQ_WAIT_ANY SQ_INSTS_LDS
@@ -22,7 +22,7 @@ mkdir -p $O
 B="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt2 -o kt -- $B > $O/kt2.log 2>&1
 echo "kt2 ok"
-RTAMD_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt1 -o kt -- $B > $O/kt1.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt1 -o kt -- $B --lanes 1 > $O/kt1.log 2>&1
 echo "kt1 ok"
 P="$B --no-profile-events"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o f -- $P > $O/fetch.log 2>&1
