@@ -29,6 +29,7 @@
 // draw counter, consumed in the reference's order.
 #include <hip/hip_runtime.h>
 #include "rt_device.h"
+#include "rt_libm.h"
 #include <cstdlib>
 
 namespace rtamd {
@@ -108,6 +109,22 @@ __device__ __forceinline__ double div_ia(const double x, const double a, const d
 }
 
 // ------------------------------------------------------------ vec.scm
+// sin / cos as the reference's libm computes them (rt_libm.h); OCML beyond the
+// reference algorithm's reduction range, which no argument on the path reaches
+__device__ __forceinline__ double rt_sin(const double x) { return rtlibm::sin_(x); }
+__device__ __forceinline__ double rt_cos(const double x) { return rtlibm::cos_(x); }
+// cos(a) and sin(b), one evaluation after the other: inlined side by side, the two would hold their
+// temporaries at once (the shade kernels' register budget)
+__device__ __forceinline__ void rt_cos_sin(const double a, const double b, double& c, double& s, const double* tab) {
+    double v0 = 0.0, v1 = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < 2; ++j) {
+        const double v = rtlibm::sincos_(j == 0 ? a : b, j == 0, tab);
+        if (j == 0) v0 = v; else v1 = v;
+    }
+    c = v0;
+    s = v1;
+}
 struct v3 { double x, y, z; };
 __device__ __forceinline__ v3 mk(double x, double y, double z) { return v3{x, y, z}; }
 __device__ __forceinline__ v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -251,8 +268,8 @@ __device__ __forceinline__ void bez_ray(const v3 o, const v3 d, BezRay& R) {
     const double dd = sqrt(lx * lx + lz * lz);
     double r[9];
     if (dd == 0.0) {
-        const double ang = (ly >= 0.0) ? -(kPi / 2) : (kPi / 2);
-        const double cs = cos(ang), sn = sin(ang);
+        // ang = -pi/2 or pi/2: libm's cos / sin of those doubles (rt_libm.h), as constants
+        const double cs = 0x1.1a62633145c07p-54, sn = (ly >= 0.0) ? -1.0 : 1.0;
         r[0] = 1.0; r[1] = 0.0; r[2] = 0.0;
         r[3] = 0.0; r[4] = cs;  r[5] = -sn;
         r[6] = 0.0; r[7] = sn;  r[8] = cs;
@@ -317,11 +334,50 @@ __device__ __forceinline__ bool bez_culled(const Bez4& c, const double w1, const
     const double ymx = fmax(fmax(c.p0.y, c.p1.y), fmax(c.p2.y, c.p3.y)) + w1;
     return zmn >= t || zmx <= 0.000001 || xmn >= w1 || xmx <= -w1 || ymn >= w1 || ymx <= -w1;
 }
-// the whole curve's cull: false => converge reports no hit for this t-max
-__device__ __forceinline__ bool bez_root_passes(const BezierRec& B, const BezRay& R, const double tmax) {
-    Bez4 c;
-    bez_load(B, R, c);
-    return !bez_culled(c, B.w1, tmax);
+// Hull culls (not in the reference; they change no result, only the work).
+// converge reports a leaf hit only at a point p = (bez-p leaf v) with
+// |p.xy|^2 < width2 (bezier.scm:156-164); v lies in [0, 1], so p is a convex
+// combination of the leaf's control points, and every sub-curve's control
+// points are convex combinations of its parent's (split, :78-87): p lies in
+// the convex hull of every ancestor's control points.  A node whose hull (in
+// the ray-space xy plane) stays farther than width1 from the ray axis
+// therefore holds no hit, and neither walking it nor culling it changes the
+// answer.  The box cull above keeps many such nodes (the box of a diagonal
+// curve is mostly empty: at C5 two thirds of the root-box survivors).  The
+// test is a separating axis: the normal of a hull edge along which every
+// control point lies more than r from the origin.  The computed points drift
+// from the exact sub-curves by a few ulps of their magnitude s per level (and
+// bez-p by a few more), so r = width1 (1 + 1e-9) + 1e-9 s keeps the cull
+// conservative by orders of magnitude; NaNs and a zero edge never cull.
+#ifndef RT_BEZ_HULL
+#define RT_BEZ_HULL 1
+#endif
+__device__ __forceinline__ bool bez_sep_axis(const Bez4& c, const v3 a, const v3 b, const double r2) {
+    const double nx = a.y - b.y, ny = b.x - a.x;                 // normal of the edge a -> b
+    const double d0 = fma(c.p0.x, nx, c.p0.y * ny), d1 = fma(c.p1.x, nx, c.p1.y * ny);
+    const double d2 = fma(c.p2.x, nx, c.p2.y * ny), d3 = fma(c.p3.x, nx, c.p3.y * ny);
+    const double mn = fmin(fmin(d0, d1), fmin(d2, d3)), mx = fmax(fmax(d0, d1), fmax(d2, d3));
+    const double lim = r2 * fma(nx, nx, ny * ny);
+    return (mn > 0.0 && mn * mn > lim) || (mx < 0.0 && mx * mx > lim);
+}
+// EDGES = 1: the chord p0 -> p3 only (the walk's splits: sub-curves are nearly
+// straight); 4: the chord and the three legs of the control polygon (roots)
+template <int EDGES>
+__device__ __forceinline__ bool bez_hull_culled(const Bez4& c, const double w1) {
+    if (!RT_BEZ_HULL) return false;
+    const double s = fmax(fmax(fmax(fabs(c.p0.x), fabs(c.p0.y)), fmax(fabs(c.p1.x), fabs(c.p1.y))),
+                          fmax(fmax(fabs(c.p2.x), fabs(c.p2.y)), fmax(fabs(c.p3.x), fabs(c.p3.y))));
+    const double r = fma(w1, 1e-9, w1) + 1e-9 * s;
+    const double r2 = r * r;
+    bool sep = bez_sep_axis(c, c.p0, c.p3, r2);
+    if (EDGES > 1)
+        sep = sep || bez_sep_axis(c, c.p0, c.p1, r2) || bez_sep_axis(c, c.p1, c.p2, r2) || bez_sep_axis(c, c.p2, c.p3, r2);
+    return sep;
+}
+// converge's box cull plus the hull cull
+template <int EDGES>
+__device__ __forceinline__ bool bez_culled_hull(const Bez4& c, const double w1, const double t) {
+    return bez_culled(c, w1, t) || bez_hull_culled<EDGES>(c, w1);
 }
 
 // The subdivision walk of converge (bezier.scm:121-175) as a per-lane state
@@ -416,15 +472,15 @@ __device__ __forceinline__ bool bez_walk_split(BezWalk& s) {
     if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
     Bez4 l, r;
     bez_split(s.c, l, r);                                       // split, left first (:167-175)
-    // (:123-128) with the best z so far
-    const bool kl = !bez_culled(l, s.w1, s.best), kr = !bez_culled(r, s.w1, s.best);
     if (!s.fresh) {                                             // one level toward the right sibling (L, idx)
         const bool right = (s.idx >> (s.L - 1 - s.rl)) & 1u;
         s.c = right ? r : l;
         if (++s.rl < s.L) return false;
-        if (right ? kr : kl) { s.fresh = true; return false; }  // it survives the cull: visit it
-        return bez_walk_next(s);
+        if (!bez_culled(s.c, s.w1, s.best)) { s.fresh = true; return false; }  // it survives the cull: visit it
+        return bez_walk_next(s);                                // (its hull passed at its first split)
     }
+    // (:123-128) with the best z so far
+    const bool kl = !bez_culled_hull<1>(l, s.w1, s.best), kr = !bez_culled_hull<1>(r, s.w1, s.best);
     if (kl || kr) {
         ++s.L;
         if (kl) {
@@ -518,7 +574,7 @@ __device__ __forceinline__ void bez_walk_take(BezWalk& s, const BezierRec& B, co
 __device__ __forceinline__ bool bezier_test(const BezierRec& B, const BezRay& R, const double tmax, double& tout) {
     Bez4 c;
     bez_load(B, R, c);
-    if (bez_culled(c, B.w1, tmax)) return false;
+    if (bez_culled_hull<4>(c, B.w1, tmax)) return false;
     const int maxd = bez_maxd(c, B.eps8);
     // converge has no depth limit (bezier.scm:189-193); a curve needing more
     // levels than the walk's 32-bit node index holds fails the render loudly
@@ -617,7 +673,7 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
             const BezierRec& B = sc.bez[e >> 6];
             Bez4 c;
             bez_load(B, W.ray[e & 63u], c);
-            keep = !bez_culled(c, B.w1, W.cl[e & 63u]);
+            keep = !bez_culled_hull<4>(c, B.w1, W.cl[e & 63u]);
             // leaf level maxd + 1, at least 0: a flat curve's maxd is negative (its root is a leaf);
             // converge has no depth limit (bezier.scm:189-193): deeper than the walk supports fails loudly
             if (keep) {
@@ -2156,7 +2212,11 @@ __device__ __forceinline__ bool checker_odd(const v3 p) {
     bool sure = true;
     const bool nx = sin_sign_neg(x, sure), ny = sin_sign_neg(y, sure), nz = sin_sign_neg(z, sure);
     if (sure) return (nx != ny) != nz;
-    const double sines = sin(x) * sin(y) * sin(z);
+    // the rare case (an argument within 1e-12 of a multiple of pi): the product itself, (sin x sin y) sin z,
+    // one sine at a time (three inlined sines side by side would hold their temporaries all at once)
+    double sines = 1.0;
+#pragma unroll 1
+    for (int i = 0; i < 3; ++i) sines = sines * rt_sin(i == 0 ? x : (i == 1 ? y : z));
     return sines < 0.0;
 }
 
@@ -2176,7 +2236,7 @@ __device__ __forceinline__ v3 tex_value(const DevScene& sc, const PerlinLds& P, 
             return mk(1.0, 1.0, 1.0) * nz;
         }
         // TEX_MARBLE :30-34
-        const double m = 0.5 * (1.0 + sin(t.scale * p.z + 10.0 * perlin_turb(P, p)));
+        const double m = 0.5 * (1.0 + rt_sin(t.scale * p.z + 10.0 * perlin_turb(P, p)));
         return mk(1.0, 1.0, 1.0) * m;
     }
     return mk(0.0, 0.0, 0.0);
@@ -2249,7 +2309,7 @@ __device__ __forceinline__ v3 random_to_sphere(const double radius, const double
     const double r2 = g.next();
     const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / distance_squared) - 1.0);
     const double phi = 2.0 * kPi * r1;
-    return mk(cos(phi) * sqrt(1.0 - z * z), sin(phi) * sqrt(1.0 - z * z), z);
+    return mk(rt_cos(phi) * sqrt(1.0 - z * z), rt_sin(phi) * sqrt(1.0 - z * z), z);
 }
 __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g) {
     if (L.type == LIGHT_RECT) {
@@ -2278,10 +2338,12 @@ __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g
 // LS = false compiles the light-sampling mixture (f2) out: scenes without a
 // light target never take it, and its constants cost scalar registers.
 // leaves: the leaf records (LDS in k_shade when the table is small, else HBM)
+// trig: rt_libm.h's sin / cos table for the lambertian bounce (an LDS copy in k_shade)
 template <int MATF, bool PN = true, bool LS = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
                                           PathRegs& p, const double t, const int32_t leaf, v3& L,
-                                          const LeafInfo* __restrict__ leaves) {
+                                          const LeafInfo* __restrict__ leaves,
+                                          const double* __restrict__ trig = rtlibm::kSinCosTab) {
     L = mk(0.0, 0.0, 0.0);
     const LeafInfo& li = leaves[leaf];                       // one record: geometry, material, texture (fields read where used)
     v3 o = p.o, d = p.d;
@@ -2339,8 +2401,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
             const double r3 = g.next(), r4 = g.next();
             (void)g.next();
             const double r6 = g.next();
-            const double x = cos(2.0 * kPi * r1) * 2.0 * sqrt(r2);
-            const double y = sin(2.0 * kPi * r3) * 2.0 * sqrt(r4);
+            double c1, s3;
+            rt_cos_sin(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
+            const double x = c1 * 2.0 * sqrt(r2);
+            const double y = s3 * 2.0 * sqrt(r4);
             const double z = sqrt(1.0 - r6);
             dir = (axis0 * x + axis1 * y) + axis2 * z;
         }
@@ -2370,8 +2434,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         const double r3 = g.next(), r4 = g.next();
         (void)g.next();
         const double r6 = g.next();
-        const double x = cos(2.0 * kPi * r1) * 2.0 * sqrt(r2);
-        const double y = sin(2.0 * kPi * r3) * 2.0 * sqrt(r4);
+        double c1, s3;
+        rt_cos_sin(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
+        const double x = c1 * 2.0 * sqrt(r2);
+        const double y = s3 * 2.0 * sqrt(r4);
         const double z = sqrt(1.0 - r6);
         const v3 target = (axis0 * x + axis1 * y) + axis2 * z;   // onb `local`
         const v3 sd = unit(target);
@@ -2458,14 +2524,19 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
                                                                 const uint32_t depth) {
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ uint32_t s_cnt[16 + 1];
+    // the lambertian bounce's sin / cos table (rt_libm.h) in LDS: its lookups are gathers
+    constexpr bool kTrig = MAT == MAT_LAMBERTIAN;
+    __shared__ double s_trig[kTrig ? 4 * 112 : 2];
+    if (kTrig)
+        for (int k = threadIdx.x; k < 4 * 112; k += 256) s_trig[k] = rtlibm::kSinCosTab[k];
     // dynamic LDS: the leaf records (LL), then the Perlin tables (PN) — only
     // what the scene uses, so the block's LDS does not cap the occupancy
     extern __shared__ uint4 s_leafdyn[];
     LeafInfo* s_leaves = reinterpret_cast<LeafInfo*>(s_leafdyn);
     PerlinLds& P = *reinterpret_cast<PerlinLds*>(s_leafdyn + (LL ? (size_t)sc.n_leaves * sizeof(LeafInfo) / 16 : 0));
     if (LL) stage_lds(s_leaves, sc.leaves, sc.n_leaves, 256);
-    stage_perlin<PN>(sc, P);                         // (its barrier also covers the leaf staging)
-    if (LL && !(PN && sc.has_perlin)) __syncthreads();
+    stage_perlin<PN>(sc, P);                         // (its barrier also covers the leaf and table staging)
+    if ((LL || kTrig) && !(PN && sc.has_perlin)) __syncthreads();
     const LeafInfo* leaves = LL ? s_leaves : sc.leaves;
     const QMap qm = qmap(qv);
     uint32_t n = 0;
@@ -2480,7 +2551,7 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
             const HitRec H = hq[qphys(qm, k)];
             load_path(in, H.slot, p, rp, depth);
             v3 L;
-            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves);
+            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves, kTrig ? s_trig : rtlibm::kSinCosTab);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);

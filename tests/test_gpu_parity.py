@@ -87,7 +87,7 @@ def _schedule(ctx, schedule):
     k_extend_lds / k_shade with sharded compaction (these small renders would
     otherwise fit under the tail threshold and run in k_finish only)."""
     if schedule == "wavefront":
-        sched.set_option("tail_off", 1)
+        ctx.set_option("tail_off", 1)
 
 
 SCHEDULES = ["tail", "wavefront"]
@@ -210,9 +210,7 @@ def test_device_resolve_matches_host(sched):
     acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
     gpu.render_device(scene, nx, ny, 0, 4, SEED, acc.data_ptr())
     out = torch.zeros(nx * ny * 3, dtype=torch.uint8, device="cuda")
-    from rtamd._lib import call
-    call("rt_resolve_u8_device", gpu_ctx.handle, ctypes.c_void_p(acc.data_ptr()), nx, ny, 4,
-         ctypes.c_void_p(out.data_ptr()), None)
+    gpu.resolve_u8_device(acc.data_ptr(), nx, ny, 4, out.data_ptr(), ctx=sched)
     host = gpu.resolve_u8(acc.cpu().numpy(), nx, ny, 4)
     assert np.array_equal(out.cpu().numpy(), host)
 
