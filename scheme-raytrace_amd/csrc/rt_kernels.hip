@@ -125,6 +125,21 @@ __device__ __forceinline__ void rt_cos_sin(const double a, const double b, doubl
     c = v0;
     s = v1;
 }
+// The bounce directions' cos / sin (random-cosine-direction, util.scm:37-44; the light mixture's
+// random-to-sphere): EX = libm's own bits (rt_libm.h), else OCML's (within 1 ulp).  Scenes with curves
+// take EX: a grazing ribbon hit turns a 1-ulp direction change into another path (the dense flat-curve
+// test); elsewhere OCML's ulps move pixels by ~1e-16 (C2 band RMS 1.6e-13) and EX would cost C2 ~4.5 %
+// (profiles/r04/ab_libm_c2.log).  Marble textures use rt_libm.h in every scene (checker_odd needs
+// only a sine's sign).
+template <bool EX>
+__device__ __forceinline__ void bounce_cos_sin(const double a, const double b, double& c, double& s, const double* tab) {
+    if (EX) {
+        rt_cos_sin(a, b, c, s, tab);
+    } else {
+        c = cos(a);
+        s = sin(b);
+    }
+}
 struct v3 { double x, y, z; };
 __device__ __forceinline__ v3 mk(double x, double y, double z) { return v3{x, y, z}; }
 __device__ __forceinline__ v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -2212,11 +2227,10 @@ __device__ __forceinline__ bool checker_odd(const v3 p) {
     bool sure = true;
     const bool nx = sin_sign_neg(x, sure), ny = sin_sign_neg(y, sure), nz = sin_sign_neg(z, sure);
     if (sure) return (nx != ny) != nz;
-    // the rare case (an argument within 1e-12 of a multiple of pi): the product itself, (sin x sin y) sin z,
-    // one sine at a time (three inlined sines side by side would hold their temporaries all at once)
-    double sines = 1.0;
-#pragma unroll 1
-    for (int i = 0; i < 3; ++i) sines = sines * rt_sin(i == 0 ? x : (i == 1 ? y : z));
+    // the rare case (an argument within 1e-12 of a multiple of pi): the product itself.  Only its sign is
+    // used, and any faithful sine (OCML's as libm's) has the exact sine's sign for a double argument (no
+    // nonzero double is a multiple of pi), so the product's sign is libm's
+    const double sines = sin(x) * sin(y) * sin(z);
     return sines < 0.0;
 }
 
@@ -2304,13 +2318,15 @@ __device__ __forceinline__ double light_pdf_value(const DevLight& L, const v3 o,
     const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
     return 1.0 / solid_angle;
 }
+template <bool EX>
 __device__ __forceinline__ v3 random_to_sphere(const double radius, const double distance_squared, Rng& g) {
     const double r1 = g.next();
     const double r2 = g.next();
     const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / distance_squared) - 1.0);
     const double phi = 2.0 * kPi * r1;
-    return mk(rt_cos(phi) * sqrt(1.0 - z * z), rt_sin(phi) * sqrt(1.0 - z * z), z);
+    return mk((EX ? rt_cos(phi) : cos(phi)) * sqrt(1.0 - z * z), (EX ? rt_sin(phi) : sin(phi)) * sqrt(1.0 - z * z), z);
 }
+template <bool EX>
 __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g) {
     if (L.type == LIGHT_RECT) {
         const double a = L.a0 + g.next() * (L.a1 - L.a0);
@@ -2324,9 +2340,9 @@ __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g
     const v3 aa = (fabs(w.x) > 0.9) ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
     const v3 vv = unit(cross(w, aa));
     const v3 uu = cross(w, vv);
-    const double x = random_to_sphere(L.r, distance_squared, g).x;      // local: three evaluations (Q29)
-    const double y = random_to_sphere(L.r, distance_squared, g).y;
-    const double z = random_to_sphere(L.r, distance_squared, g).z;
+    const double x = random_to_sphere<EX>(L.r, distance_squared, g).x;  // local: three evaluations (Q29)
+    const double y = random_to_sphere<EX>(L.r, distance_squared, g).y;
+    const double z = random_to_sphere<EX>(L.r, distance_squared, g).z;
     return (uu * x + vv * y) + w * z;
 }
 
@@ -2339,7 +2355,7 @@ __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g
 // light target never take it, and its constants cost scalar registers.
 // leaves: the leaf records (LDS in k_shade when the table is small, else HBM)
 // trig: rt_libm.h's sin / cos table for the lambertian bounce (an LDS copy in k_shade)
-template <int MATF, bool PN = true, bool LS = true>
+template <int MATF, bool PN = true, bool LS = true, bool EX = true>
 __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P, const RenderParams& rp,
                                           PathRegs& p, const double t, const int32_t leaf, v3& L,
                                           const LeafInfo* __restrict__ leaves,
@@ -2395,14 +2411,14 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         const DevLight& Lt = sc.light;
         v3 dir;
         if (g.next() < 0.5) {
-            dir = light_random(Lt, pt, g);
+            dir = light_random<EX>(Lt, pt, g);
         } else {
             const double r1 = g.next(), r2 = g.next();
             const double r3 = g.next(), r4 = g.next();
             (void)g.next();
             const double r6 = g.next();
             double c1, s3;
-            rt_cos_sin(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
+            bounce_cos_sin<EX>(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
             const double x = c1 * 2.0 * sqrt(r2);
             const double y = s3 * 2.0 * sqrt(r4);
             const double z = sqrt(1.0 - r6);
@@ -2435,7 +2451,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
         (void)g.next();
         const double r6 = g.next();
         double c1, s3;
-        rt_cos_sin(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
+        bounce_cos_sin<EX>(2.0 * kPi * r1, 2.0 * kPi * r3, c1, s3, trig);
         const double x = c1 * 2.0 * sqrt(r2);
         const double y = s3 * 2.0 * sqrt(r4);
         const double z = sqrt(1.0 - r6);
@@ -2516,7 +2532,7 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 #endif
 template <int MAT>
 constexpr int shade_waves() { return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD : RT_SHADE_WAVES; }
-template <int MAT, bool PN, bool LS, bool LL>
+template <int MAT, bool PN, bool LS, bool LL, bool EX>
 __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
                                                                 const PathState in, const HitRec* __restrict__ hq,
                                                                 const QView qv, PathState out,
@@ -2525,7 +2541,7 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
     const DevScene& sc = *scp;                       // scene in device memory: fields load on demand
     __shared__ uint32_t s_cnt[16 + 1];
     // the lambertian bounce's sin / cos table (rt_libm.h) in LDS: its lookups are gathers
-    constexpr bool kTrig = MAT == MAT_LAMBERTIAN;
+    constexpr bool kTrig = MAT == MAT_LAMBERTIAN && EX;
     __shared__ double s_trig[kTrig ? 4 * 112 : 2];
     if (kTrig)
         for (int k = threadIdx.x; k < 4 * 112; k += 256) s_trig[k] = rtlibm::kSinCosTab[k];
@@ -2551,7 +2567,7 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
             const HitRec H = hq[qphys(qm, k)];
             load_path(in, H.slot, p, rp, depth);
             v3 L;
-            alive = shade_hit<MAT, PN, LS>(sc, P, rp, p, H.t, H.leaf, L, leaves, kTrig ? s_trig : rtlibm::kSinCosTab);
+            alive = shade_hit<MAT, PN, LS, EX>(sc, P, rp, p, H.t, H.leaf, L, leaves, kTrig ? s_trig : rtlibm::kSinCosTab);
             if (!alive) write_sample(rp, p, L);
         }
         const uint32_t slot = block_append<1>(alive ? 0 : -1, out_counts, shard_cap, s_cnt);
@@ -2652,7 +2668,7 @@ __global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(co
             v3 L;
             bool cont = false;
             if (leaf < 0) L = sky_radiance(sc, p.d);
-            else cont = shade_hit<-1, PN, LSM>(sc, P, rp, p, t, leaf, L, sc.leaves);
+            else cont = shade_hit<-1, PN, LSM, (F & kFeatCurves) != 0>(sc, P, rp, p, t, leaf, L, sc.leaves);
             if (!cont) { write_sample(rp, p, L); active = false; }
         }
     }
@@ -2844,14 +2860,21 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks == 0u) blocks = kShards;
     const HitRec* hq = hit.h + (size_t)mat * hit.stride;
-#define RT_SHADE(M, PN, LS)                                                                                  \
+#define RT_SHADE_EX(M, PN, LS, EX)                                                                           \
     do {                                                                                                     \
         if (ll)                                                                                              \
-            hipLaunchKernelGGL((k_shade<M, PN, LS, true>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hq,   \
-                               qv, out, out_counts, shard_cap, depth);                                       \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, true, EX>), dim3(blocks), dim3(256), lds, s, scd, rp, in,   \
+                               hq, qv, out, out_counts, shard_cap, depth);                                   \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_shade<M, PN, LS, false>), dim3(blocks), dim3(256), lds, s, scd, rp, in, hq,  \
-                               qv, out, out_counts, shard_cap, depth);                                       \
+            hipLaunchKernelGGL((k_shade<M, PN, LS, false, EX>), dim3(blocks), dim3(256), lds, s, scd, rp, in,  \
+                               hq, qv, out, out_counts, shard_cap, depth);                                   \
+    } while (0)
+    // libm's own sin / cos for the bounce directions in scenes with curves (bounce_cos_sin); only the
+    // lambertian kernels draw directions with them
+#define RT_SHADE(M, PN, LS)                                                                                  \
+    do {                                                                                                     \
+        if (M == MAT_LAMBERTIAN && sc.n_bez > 0) RT_SHADE_EX(M, PN, LS, true);                              \
+        else RT_SHADE_EX(M, PN, LS, false);                                                                  \
     } while (0)
     const bool pn = sc.has_noise_tex != 0;
     const bool ls = sc.light.type != LIGHT_OFF;       // only lambertian scatter uses the light mixture
@@ -2869,6 +2892,7 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
     default: if (pn) RT_SHADE(MAT_DIFFUSE_LIGHT, true, false); else RT_SHADE(MAT_DIFFUSE_LIGHT, false, false); break;
     }
 #undef RT_SHADE
+#undef RT_SHADE_EX
     return hipGetLastError();
 }
 hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderParams& rp, const PathState& st, const QView& in,

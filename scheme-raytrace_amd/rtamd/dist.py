@@ -11,9 +11,9 @@ ships 1/world of the frame instead of a full-frame buffer, and the result is
 bit-identical to a one-process render (the pixels are disjoint, nothing is
 summed).
 
-``gather_frame`` is the exchange step; bench.py calls it through
-``render_frame`` on the GPU, tests/test_distributed.py calls it with gloo on
-CPU tensors.
+``gather_frame`` is the exchange step; bench.py calls it after each rank's
+rt_render_shard_device (timing the two apart), tests/test_distributed.py calls
+it with gloo on CPU tensors.
 """
 import numpy as np
 
@@ -33,17 +33,21 @@ def shard_pixels(nx, ny, world):
 
 def _gather_buffers(nx, ny, world, dtype, dev, frame_dev):
     """The exchange's buffers, made once per (frame, world, device) and kept:
-    the padded send buffer, rank 0's receive buffers, and every rank's pixel
-    index list already on rank 0's device (no host upload per frame)."""
+    the padded send buffer, rank 0's receive buffer (one tensor, a row per
+    rank), and the scatter's two index lists already on rank 0's device: the
+    receive rows' valid pixels (padding skipped) and their frame pixels."""
     import torch
     key = (nx, ny, world, dtype, str(dev), str(frame_dev))
     if key not in _dev_cache:
         pix = shard_pixels(nx, ny, world)
-        width = 3 * max(len(p) for p in pix)    # collectives move equal-size buffers: pad to the largest shard
+        width = max(len(p) for p in pix)        # collectives move equal-size buffers: pad to the largest shard
+        src = np.concatenate([r * width + np.arange(len(p), dtype=np.int64) for r, p in enumerate(pix)])
+        dst = np.concatenate(pix)
         _dev_cache[key] = {
-            "send": torch.zeros(width, dtype=dtype, device=dev),
+            "send": torch.zeros(3 * width, dtype=dtype, device=dev),
             "recv": None,                       # rank 0 only (gather_frame)
-            "idx": [torch.from_numpy(p).to(frame_dev) for p in pix],
+            "src": torch.from_numpy(src).to(frame_dev), "dst": torch.from_numpy(dst).to(frame_dev),
+            "width": width,
         }
     return _dev_cache[key]
 
@@ -53,7 +57,8 @@ def gather_frame(local, nx, ny, rank, world, group=None, out=None):
     3 x its pixel count) onto rank 0 and scatter it into an nx*ny*3 frame
     (``out`` if given, else a new tensor on local's device).  Returns the
     frame on rank 0, None on other ranks.  Shards differ by at most one
-    16x16 tile, so padding them to equal size moves < 6 KB more per rank."""
+    16x16 tile, so padding them to equal size moves < 6 KB more per rank;
+    rank 0 then places all of them with one gather and one scatter."""
     import torch
     import torch.distributed as dist
 
@@ -68,17 +73,16 @@ def gather_frame(local, nx, ny, rank, world, group=None, out=None):
     send = B["send"]
     send[:local.numel()].copy_(local)
     if rank == 0 and B["recv"] is None:
-        B["recv"] = [torch.empty_like(send) for _ in range(world)]
-    dist.gather(send, gather_list=B["recv"] if rank == 0 else None, dst=0, group=group)
+        B["recv"] = torch.empty(world, send.numel(), dtype=send.dtype, device=dev)
+    dist.gather(send, gather_list=list(B["recv"].unbind(0)) if rank == 0 else None, dst=0, group=group)
     if rank != 0:
         return None
     if out is None:
         out = torch.empty(nx * ny * 3, dtype=local.dtype, device=local.device)
     if out.numel() != nx * ny * 3:
         raise ValueError("out must hold nx*ny*3 values")
-    rows = out.view(-1, 3)                      # the shards cover every pixel exactly once
-    for r in range(world):
-        rows.index_copy_(0, B["idx"][r], B["recv"][r][:3 * counts[r]].view(-1, 3).to(local.device))
+    recv = B["recv"].to(local.device).view(-1, 3)     # the shards cover every pixel exactly once
+    out.view(-1, 3).index_copy_(0, B["dst"], recv.index_select(0, B["src"]))
     return out
 
 

@@ -68,23 +68,23 @@ def test_c5_band_production_vs_oracle(sched, oracle_mod):
           % (y0, y0 + rows - 1, s0, s0 + n - 1, rms, dmax, nbad, npx, st.segments, segs, st.chunks, st.lanes,
              st.curve_pooled_batches))
     assert rms <= RMS_TOL
-    assert nbad <= max(2, npx // 200)
+    assert nbad <= 2
     assert not got[:3 * lo].any() and not got[3 * hi:].any()
 
 
-def _flat_curve_scene(nx, ny):
-    """The Cornell frame with 20 000 short curves (extent ~0.5, width 3) in
-    front of the camera: half straight (l0 is rounding only, converge's depth
-    estimate ~ -20), half bent by ~1e-3 (depth -2..-4): every root is a leaf.
-    Sparse enough that paths are short: in a denser cloud (200 000 curves of
-    width 6) ribbons graze each other so often that the 1-ulp differences of
-    OCML's sin / cos from glibc's flip whole paths (a 1-ulp change of every
-    oracle cos alone changes 0.7 % of that scene's pixels)."""
+def _flat_curve_scene(nx, ny, m=20000, width=3.0):
+    """The Cornell frame with m short curves (extent ~0.5) in front of the
+    camera: half straight (l0 is rounding only, converge's depth estimate
+    ~ -20), half bent by ~1e-3 (depth -2..-4): every root is a leaf.  With
+    200 000 curves of width 6 the ribbons overlap so often that grazing
+    bounces decide most paths: until round 4 a 1-ulp difference of the
+    device's sin / cos from the C library's (a lambertian bounce direction,
+    util.scm:37-44) changed 0.7 % of that scene's pixels; the device now
+    computes libm's own bits (rt_libm.h)."""
     rs = np.random.default_rng(0x5EED0105)
     white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
     red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
     light = g.make_diffuse_light(g.constant_texture(v.vec3(4, 4, 4)))
-    m = 20000
     base = rs.uniform(150.0, 400.0, size=(m, 1, 3))
     t = np.linspace(0.0, 0.5, 4).reshape(1, 4, 1) * rs.normal(size=(m, 1, 3))
     bend = 1e-3 * rs.normal(size=(m, 4, 3))
@@ -93,28 +93,32 @@ def _flat_curve_scene(nx, ny):
             g.make_yz_rect(0, 555, 0, 555, 0, red),
             g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)),
             g.make_xz_rect(0, 555, 0, 555, 0, white),
-            g.make_bvh_node([g.bezier_array((base + t + bend).reshape(m, 12), 3.0, white)], 0, 0)]
+            g.make_bvh_node([g.bezier_array((base + t + bend).reshape(m, 12), width, white)], 0, 0)]
     return g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
 
 
-def test_flat_curves_in_pooled_batches_vs_oracle(sched, oracle_mod):
+@pytest.mark.parametrize("m,width", [(20000, 3.0), (200000, 6.0)])
+def test_flat_curves_in_pooled_batches_vs_oracle(sched, oracle_mod, m, width):
     """Flat curves reach the pooled stage B of k_extend_curves (counted on the
-    device), the render raises no fault, and the image matches the oracle."""
-    nx, ny, spp = 128, 128, 64          # a flipped sample moves its pixel by ~1e-2 / spp
-    sc = _flat_curve_scene(nx, ny)
+    device), the render raises no fault, and the image matches the oracle:
+    at most 2 of 16 384 pixels above 1e-9 (a flipped sample moves its pixel by
+    ~1e-2 / spp), in the sparse cloud and in the dense one."""
+    nx, ny, spp = 128, 128, 64
+    sc = _flat_curve_scene(nx, ny, m, width)
     _opts(sched, tail_off=1, lanes=1)
     acc = np.zeros(nx * ny * 3)
     h = gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
     st = gpu.stats(h)
-    print("flat curves: pooled batches %d, flat survivors walked in them %d, segments %d"
-          % (st.curve_pooled_batches, st.curve_flat_pooled, st.segments))
+    print("flat curves (%d, width %g): pooled batches %d, flat survivors walked in them %d, segments %d"
+          % (m, width, st.curve_pooled_batches, st.curve_flat_pooled, st.segments))
     assert st.finish_paths == 0
     assert st.curve_pooled_batches > 0 and st.curve_flat_pooled > 0
-    ref, _ = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=host_threads())
+    ref, segs = oracle_mod.build_scene(sc).render(nx, ny, 0, spp, SEED, nthreads=host_threads())
     rms, dmax, nbad, npx = _compare(acc, ref, spp)
-    print("flat curves vs oracle: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
+    print("flat curves (%d, width %g) vs oracle: rms=%.3e max=%.3e pixels>1e-9: %d/%d segments gpu %d oracle %d"
+          % (m, width, rms, dmax, nbad, npx, st.segments, segs))
     assert rms <= RMS_TOL
-    assert nbad <= max(2, npx // 200)
+    assert nbad <= 2
     # the same render through the tail kernel's per-lane curve test: bit for bit
     _opts(sched, tail_off=0, tail_paths=100000000)
     b = np.zeros(nx * ny * 3)
@@ -181,7 +185,7 @@ def test_duplicate_curves_tie_to_the_later_curve(sched, oracle_mod):
     ref, _ = o.render(nx, ny, 0, 4, SEED, nthreads=host_threads())
     rms, dmax, nbad, npx = _compare(acc, ref, 4)
     print("duplicate curves render: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
-    assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
+    assert rms <= RMS_TOL and nbad <= 2
 
 
 def test_few_curves_among_spheres_large_launch(sched, oracle_mod, monkeypatch):
@@ -219,7 +223,7 @@ def test_few_curves_among_spheres_large_launch(sched, oracle_mod, monkeypatch):
     rms, dmax, nbad, npx = _compare(acc[3 * lo:3 * hi], ref[3 * lo:3 * hi], spp)
     print("few curves among spheres: segments %d, rows %d..%d vs oracle rms=%.3e max=%.3e pixels>1e-9: %d/%d"
           % (st.segments, y0, y0 + rows - 1, rms, dmax, nbad, npx))
-    assert rms <= RMS_TOL and nbad <= max(2, npx // 200)
+    assert rms <= RMS_TOL and nbad <= 2
 
 
 def test_curve_walk_stack_overflow_bitwise(sched, monkeypatch):
