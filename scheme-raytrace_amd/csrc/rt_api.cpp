@@ -91,7 +91,11 @@ struct DevBuf {
 // long, narrow tail of one chunk (its last few paths bouncing to depth 100)
 // overlaps the wide first iterations of the next one instead of leaving the
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
-constexpr int kLanes = 4;                  // most lanes a render may use (RTAMD_LANES)
+constexpr int kLanes = 4;                  // most lanes a render may use (RT_OPT_LANES)
+#ifndef RT_CURVE_LDS_STACK
+#define RT_CURVE_LDS_STACK 8
+#endif
+constexpr int kCurveLdsStack = RT_CURVE_LDS_STACK;   // k_extend_curves' BVH4 stack entries in LDS per lane
 struct Lane {
     DevBuf st_a, st_b, hit, sb, counts, seg_tail;
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
@@ -998,6 +1002,8 @@ int commit_scene(Scene* s, int world) {
     if (int rc = upload(s->d_bgroups, bgroups, &d.bgroups)) return rc;
     d.n_bgroups = (int)bgroups.size();
     d.bvh_has_bez = bvh_has_bez ? 1 : 0;
+    d.bez_groups = 0;
+    for (const Group& G : groups) d.bez_groups += G.type == LEAF_BEZIER ? 1 : 0;
     d.bvh_pad = bvh_pad;
     if (int rc = upload(s->d_bvh2, bvh2, &d.bvh2)) return rc;
     if (int rc = upload(s->d_bleaf, bleaf, &d.bleaf)) return rc;
@@ -1022,9 +1028,11 @@ int commit_scene(Scene* s, int world) {
         d.n_bvh4 = (int)bvh4.size();
         d.bvh4_root = bvh4_root;
         d.stack4 = stack4;
-        // RTAMD_CURVE_LDS_STACK (tests): fewer LDS entries, so the walk exercises its overflow area
+        // the walk's LDS stack column: kCurveLdsStack entries (a walk rarely holds more; the rest go to the
+        // overflow area), so the curve kernel's blocks stay small.  RTAMD_CURVE_LDS_STACK (tests): fewer
+        // entries, so the walk exercises its overflow area
         const char* ce = std::getenv("RTAMD_CURVE_LDS_STACK");
-        d.lds4 = ce ? std::max(1, std::min(lane_stack, std::atoi(ce))) : lane_stack;
+        d.lds4 = std::min(lane_stack, ce ? std::max(1, std::atoi(ce)) : kCurveLdsStack);
         if (stack4 > d.lds4) {                       // the walk's deepest stacks spill past the LDS columns
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
@@ -1176,7 +1184,7 @@ int lanes_wanted(const Context& c) {   // RT_OPT_LANES: path pools kept in fligh
 // Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RT_OPT_LANES overrides.
 int lanes_for(const Context& c, const DevScene& d) {
     if (c.opt_lanes > 0) return lanes_wanted(c);
-    const bool curve_kernel = d.n_bez > 0 && d.bvh_has_bez && d.n_med == 0 && d.n_klein == 0;
+    const bool curve_kernel = d.n_bez > 0 && d.bvh_has_bez && d.bez_groups == 0 && d.n_med == 0 && d.n_klein == 0;
     return curve_kernel ? 1 : lanes_wanted(c);
 }
 

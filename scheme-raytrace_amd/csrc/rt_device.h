@@ -138,6 +138,7 @@ struct DevScene {
     const BvhNode2* bvh2;  int32_t n_bvh2;
     const BvhLeaf* bleaf;  int32_t bvh2_root;      // root child ref (may be a leaf)
     int32_t bvh_has_bez;                           // curves in the BVH: widen the box t range (see bvh_closest)
+    int32_t bez_groups;                            // curve groups outside the world BVH (k_extend_curves needs none)
     float bvh_pad;                                 // the margin baked into the f32 boxes (diagnostic)
     int32_t lane_stack;                            // deepest BVH2 level (stack entries a traversal needs)
     // BVH4 of the same tree (curve trees only, else nullptr): its walk pushes up to three children per

@@ -274,7 +274,9 @@ __device__ __forceinline__ void sphere_test(const v3 o, const v3 d, const double
 // `converge` gives both children of a split the t it was called with, so the
 // curve's answer is min z over all leaf hits with z <= t; the recursion
 // becomes an explicit per-lane stack (private memory).
-struct BezRay { double m[12]; };        // rows 0..3, columns 0..2 of the 4x4 projection matrix
+// rows 0..3, columns 0..2 of the 4x4 projection matrix without its entry (1, 0), which both branches of
+// get-projection-mat make 0 (m[k] for k < 3, m[k - 1] after: 11 doubles in the wave's LDS per lane)
+struct BezRay { double m[11]; };
 
 __device__ __forceinline__ void bez_ray(const v3 o, const v3 d, BezRay& R) {
     const double ox = -o.x, oy = -(-o.z), oz = -o.y;
@@ -295,16 +297,17 @@ __device__ __forceinline__ void bez_ray(const v3 o, const v3 d, BezRay& R) {
     }
     // array-mul with the translation: rows 0..2 are the rotation, row 3 = o' R
 #pragma unroll
-    for (int k = 0; k < 9; ++k) R.m[k] = r[k];
+    for (int k = 0; k < 9; ++k) if (k != 3) R.m[k < 3 ? k : k - 1] = r[k];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) R.m[9 + j] = ((ox * r[j] + oy * r[3 + j]) + oz * r[6 + j]) + 0.0;
+    for (int j = 0; j < 3; ++j) R.m[8 + j] = ((ox * r[j] + oy * r[3 + j]) + oz * r[6 + j]) + 0.0;
 }
 // transform (bezier.scm:49-55): row vector (x, -z, y, 1) times the matrix
 __device__ __forceinline__ v3 bez_xf(const BezRay& R, const double x, const double y, const double z) {
     const double a = x, b = -z, c = y;
-    return mk(((a * R.m[0] + b * R.m[3]) + c * R.m[6]) + R.m[9],
-              ((a * R.m[1] + b * R.m[4]) + c * R.m[7]) + R.m[10],
-              ((a * R.m[2] + b * R.m[5]) + c * R.m[8]) + R.m[11]);
+    // b * 0.0 kept as an operation: it is -0 for negative b, and a * m0 + (-0) keeps a -0 product's sign
+    return mk(((a * R.m[0] + b * 0.0) + c * R.m[5]) + R.m[8],
+              ((a * R.m[1] + b * R.m[3]) + c * R.m[6]) + R.m[9],
+              ((a * R.m[2] + b * R.m[4]) + c * R.m[7]) + R.m[10]);
 }
 struct Bez4 { v3 p0, p1, p2, p3; };
 __device__ __forceinline__ v3 bez_point(const Bez4& c, const double t) {       // bez-p :67-77
@@ -376,7 +379,9 @@ __device__ __forceinline__ bool bez_sep_axis(const Bez4& c, const v3 a, const v3
     return (mn > 0.0 && mn * mn > lim) || (mx < 0.0 && mx * mx > lim);
 }
 // EDGES = 1: the chord p0 -> p3 only (the walk's splits: sub-curves are nearly
-// straight); 4: the chord and the three legs of the control polygon (roots)
+// straight); 4: the chord and the three legs of the control polygon (roots;
+// the two diagonals as well cut C5's survivors by another ~10 % in a host
+// simulation but cost more in stage A than they save: -1.2 % at 8 spp)
 template <int EDGES>
 __device__ __forceinline__ bool bez_hull_culled(const Bez4& c, const double w1) {
     if (!RT_BEZ_HULL) return false;
@@ -433,6 +438,7 @@ struct BezWalk {
     int rl;                         // re-derivation (!fresh): c is the path node at level rl < L
     uint32_t idx, it, cap;
     uint32_t rmask;                 // bit L: the right sibling of the level-L left half was culled at the split
+    int pl;                         // the level of the pending right sibling held in the lane's LDS slot (-1: none)
     bool fresh, found;              // fresh: c is node (L, idx) and passed the cull
 };
 // converge's subdivision depth from the transformed curve's flatness (:180-193)
@@ -457,7 +463,7 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
     // each of the <= 2^(leaf_level+1) nodes is visited at most once, for at
     // most leaf_level re-derivation splits and one split or leaf test
     s.cap = (uint32_t)(s.leaf_level + 2) << (s.leaf_level + 1);
-    s.L = 0; s.base = 0; s.rl = 0; s.idx = 0; s.it = 0; s.rmask = 0;
+    s.L = 0; s.base = 0; s.rl = 0; s.idx = 0; s.it = 0; s.rmask = 0; s.pl = -1;
     s.fresh = true; s.found = false; s.best = tmax;
 }
 // at a leaf segment: the next call is bez_walk_leaf
@@ -483,7 +489,12 @@ __device__ __forceinline__ bool bez_walk_next(BezWalk& s) {
     return false;
 }
 // one split (not at a leaf: !bez_walk_at_leaf); true once the walk is over
-__device__ __forceinline__ bool bez_walk_split(BezWalk& s) {
+// slot (stage B only; nullptr in the per-lane walk): the lane's LDS copy of the latest pending right
+// sibling.  Depth first, that sibling is the next pending node the walk turns to (every later one lies in
+// its left brother's subtree and is visited first), so the walk takes it from the slot instead of
+// re-deriving it from the root, bit for bit the same values; older ones are overwritten and re-derived.
+template <bool SLOT = false>
+__device__ __forceinline__ bool bez_walk_split(BezWalk& s, Bez4* slot = nullptr) {
     if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
     Bez4 l, r;
     bez_split(s.c, l, r);                                       // split, left first (:167-175)
@@ -501,6 +512,7 @@ __device__ __forceinline__ bool bez_walk_split(BezWalk& s) {
         if (kl) {
             s.c = l; s.idx <<= 1;
             s.rmask = kr ? (s.rmask & ~(1u << s.L)) : (s.rmask | (1u << s.L));
+            if (SLOT && kr) { *slot = r; s.pl = s.L; }
         } else {
             s.c = r; s.idx = (s.idx << 1) | 1u;
         }
@@ -510,21 +522,27 @@ __device__ __forceinline__ bool bez_walk_split(BezWalk& s) {
 }
 // one node (not at a leaf): a pending right sibling is re-derived from the
 // root in one go, then split; true once the walk is over
-__device__ __forceinline__ bool bez_walk_node(BezWalk& s) {
+template <bool SLOT = false>
+__device__ __forceinline__ bool bez_walk_node(BezWalk& s, Bez4* slot = nullptr) {
     if (!s.fresh) {
         if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
-        s.c = s.root;
-        for (int k = s.L - 1; k >= 0; --k) {
-            Bez4 l, r;
-            bez_split(s.c, l, r);
-            s.c = ((s.idx >> k) & 1u) ? r : l;
+        if (SLOT && s.pl == s.L) {                              // the pending sibling kept in the slot
+            s.c = *slot;
+            s.pl = -1;
+        } else {
+            s.c = s.root;
+            for (int k = s.L - 1; k >= 0; --k) {
+                Bez4 l, r;
+                bez_split(s.c, l, r);
+                s.c = ((s.idx >> k) & 1u) ? r : l;
+            }
         }
         if (bez_culled(s.c, s.w1, s.best)) return bez_walk_next(s);
         s.rl = s.L;
         s.fresh = true;
         if (s.L >= s.leaf_level) return false;                  // a leaf: tested in a leaf phase
     }
-    return bez_walk_split(s);
+    return bez_walk_split<SLOT>(s, slot);
 }
 // the leaf segment's test (:130-166) (bez_walk_at_leaf); true once the walk is over
 __device__ __forceinline__ bool bez_walk_leaf(BezWalk& s) {
@@ -573,6 +591,7 @@ __device__ __forceinline__ void bez_walk_donate(BezWalk& s, const uint32_t pend,
     l = (uint32_t)__builtin_ctz(pend);
     ridx = (s.idx >> ((uint32_t)s.L - l)) | 1u;
     s.rmask |= 1u << l;
+    if (s.pl == (int)l) s.pl = -1;                              // it is not this walk's any more
 }
 // Start a walk of the donated subtree rooted at node (l, ridx) of curve B
 // (re-derived from the root at the first step; the walk ends back at level l).
@@ -641,7 +660,7 @@ constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the
 #ifndef RT_BEZ_QFLUSH
 #define RT_BEZ_QFLUSH 48               // k_extend_curves: queued candidates that trigger a batch (stage A)
 #endif
-constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 2 * 64;   // < the trigger before a step, + 2 per lane per step
+constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 64;   // < the trigger before a step, + 1 per lane per step
 #ifndef RT_BEZ_HOLD
 #define RT_BEZ_HOLD 64                 // stage B runs once this many root-cull survivors wait (multiple of 64)
 #endif
@@ -652,6 +671,8 @@ constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 2 * 64;   // <
 #define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
 #endif
 constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
+static_assert(2 * 64 <= kBezQ, "stage B's donation handover: two words per donor lane in W.q");
+static_assert(kBezMaxDepth + 1 < 26, "the handover packs a level (6 bits) above a node index (26 bits)");
 struct BezWave {
     BezRay ray[64];                 // owner lane's ray-space matrix
     double cl[64];                  // owner's closest t when a batch runs
@@ -661,6 +682,7 @@ struct BezWave {
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
     uint32_t done[64];              // persistent kernel: owner's candidates resolved so far
+    Bez4 pend[64];                  // stage B: each lane's latest pending right sibling (bez_walk_split)
     uint8_t lev[kBezS];             // survivors' subdivision leaf levels (stage A)
 };
 __device__ __forceinline__ void wave_sync() {
@@ -748,6 +770,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
         // nodes [36] re-derivation splits [37] leaf tests [38] survivors [39] stage B clock (lane 0)
         uint32_t n_it = 0, n_busy = 0, n_step = 0, n_red = 0, n_rsplit = 0, n_leaf = 0;
         unsigned long long n_clk_refill = 0;          // [45] stage B clock in refill / donation rounds (lane 0)
+        unsigned long long n_clk_leaf = 0, n_clk_node = 0;   // [46] leaf tests, [47] node steps (splits, re-derivation)
         const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
 #endif
         const unsigned long long guard_cap = (unsigned long long)(nb + 2u) * (((unsigned long long)(kBezMaxDepth + 3) << (kBezMaxDepth + 2)) + 2ull);
@@ -787,15 +810,15 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (pend != 0u && dr < nd) {
                         uint32_t l, ridx;
                         bez_walk_donate(wk, pend, l, ridx);
-                        W.q[3 * dr] = si; W.q[3 * dr + 1] = l; W.q[3 * dr + 2] = ridx;
+                        W.q[2 * dr] = si; W.q[2 * dr + 1] = (l << 26) | ridx;     // l <= 25, ridx < 2^25
                     }
                     wave_sync();
                     const uint32_t ir = lanes_below(idle);
                     if (!busy && ir < nd) {
-                        si = W.q[3 * ir];
-                        const uint32_t e = W.sv[si];
-                        bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], W.q[3 * ir + 1],
-                                      W.q[3 * ir + 2]);
+                        si = W.q[2 * ir];
+                        const uint32_t e = W.sv[si], lr = W.q[2 * ir + 1];
+                        bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], lr >> 26,
+                                      lr & ((1u << 26) - 1u));
                         busy = true;
                     }
                     wave_sync();
@@ -814,10 +837,20 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             const bool at_leaf = busy && bez_walk_at_leaf(wk);
             const unsigned long long lm = __ballot(at_leaf);
             bool over = false;
+#ifdef RT_STATS
+            const unsigned long long cl0 = __builtin_amdgcn_s_memtime();
+#endif
             if (lm != 0ull && (__popcll(lm) >= RT_BEZ_LEAF_PHASE || lm == bm)) {
                 if (at_leaf) over = bez_walk_leaf(wk);
             }
-            if (busy && !at_leaf) over = bez_walk_node(wk);
+#ifdef RT_STATS
+            const unsigned long long cl1 = __builtin_amdgcn_s_memtime();
+            n_clk_leaf += cl1 - cl0;
+#endif
+            if (busy && !at_leaf) over = bez_walk_node<true>(wk, &W.pend[threadIdx.x & 63u]);
+#ifdef RT_STATS
+            n_clk_node += __builtin_amdgcn_s_memtime() - cl1;
+#endif
             if (over) {
                 if (wk.found)
                     atomicMin((unsigned long long*)&W.sz[si], (unsigned long long)__double_as_longlong(wk.best));
@@ -825,10 +858,23 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             }
         }
 #ifdef RT_STATS
-        RT_STAT(33, n_busy); RT_STAT(34, n_step); RT_STAT(35, n_red); RT_STAT(36, n_rsplit); RT_STAT(37, n_leaf);
+        {   // per-lane counts summed in LDS first: 64 global atomics per counter and pass would load stage B itself
+            __shared__ unsigned int s_st[4][5];
+            unsigned int* ws = s_st[(threadIdx.x >> 6) & 3u];
+            for (uint32_t j = rank; j < 5u; j += nact) ws[j] = 0u;
+            wave_sync();
+            atomicAdd(&ws[0], n_busy); atomicAdd(&ws[1], n_step); atomicAdd(&ws[2], n_red);
+            atomicAdd(&ws[3], n_rsplit); atomicAdd(&ws[4], n_leaf);
+            wave_sync();
+            if (rank == 0) {
+                RT_STAT(33, ws[0]); RT_STAT(34, ws[1]); RT_STAT(35, ws[2]); RT_STAT(36, ws[3]); RT_STAT(37, ws[4]);
+            }
+            wave_sync();
+        }
         if (rank == 0) {
             RT_STAT(31, 1); RT_STAT(32, n_it); RT_STAT(38, nb);
             RT_STAT(39, __builtin_amdgcn_s_memtime() - clk0); RT_STAT(45, n_clk_refill);
+            RT_STAT(46, n_clk_leaf); RT_STAT(47, n_clk_node);
         }
 #endif
     }
@@ -1188,9 +1234,8 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                 }
             }
         }
-        // append this step's curve candidates (at most 2 per lane)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        // append one of this lane's curve candidates (kBezQ: at most one per lane per step)
+        {
             const bool has = pb < pe;
             const unsigned long long m = __ballot(has);
             if (has) { W.q[qn + lanes_below(m)] = ((uint32_t)pb << 6) | lane; ++pb; }
@@ -1713,12 +1758,17 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // bvh_closest_curves; a ray finishes once its traversal has ended and every
 // curve candidate it queued has been resolved by a batch (W.done).
 // =====================================================================
-__global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, const RenderParams rp,
+#ifndef RT_CURVE_WAVES
+#define RT_CURVE_WAVES 2               // waves per SIMD k_extend_curves is compiled for (VGPR budget 512 / waves)
+#endif
+#ifndef RT_CURVE_PREFETCH
+#define RT_CURVE_PREFETCH 1            // load the lane's next BVH4 node one iteration ahead (32 VGPRs)
+#endif
+__global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                        const bool depth0, unsigned int* __restrict__ claim) {
-    constexpr int F = kFeatCurves;
-    extern __shared__ uint32_t s_lstack[];          // per-lane BVH stack, 256 x sc.lane_stack (dynamic LDS)
+    extern __shared__ uint32_t s_lstack[];          // per-lane BVH4 stack column, 256 x sc.lds4 (dynamic LDS)
     __shared__ BezWave s_bw[4];
     BezWave& W = s_bw[threadIdx.x >> 6];
     uint32_t* lstk = s_lstack + threadIdx.x;
@@ -1730,14 +1780,24 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
     while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
     bool active = false, exhausted = false, trav = false;
     uint32_t k = 0, i = 0, queued = 0;
-    v3 o = mk(0.0, 0.0, 0.0), d = o;
-    double tm = 0.0, a = 0.0, ia = 0.0, tscale = 1.0, closest = kTmax;
+    // The ray itself (o, d, time) is not kept in registers across iterations: the BVH step needs only
+    // its box-test form and t scale, the sphere leaves and the finish reload it (ray_of below), so stage
+    // B's walk state fits beside the loop's (registers cap the waves per SIMD, RT_CURVE_WAVES)
+    double tscale = 1.0, closest = kTmax;
     int32_t best = -1, node = 0;
     BoxRay br{};
+#if RT_CURVE_PREFETCH
     BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
+#endif
+    auto ray_of = [&](v3& o, v3& d, double& tm) {
+        const RayRec R = st.ray[i];
+        o = mk(R.ox, R.oy, R.oz);
+        d = mk(R.dx, R.dy, R.dz);
+        tm = depth0 ? st.tm[i] : 0.0;
+    };
     int sp = 0, pb = 0, pe = 0;
     // the walk's stack: LDS column for the first lds4 entries, the global overflow area past them
-    const int lds4 = sc.lds4;                       // <= lane_stack, the column's allocated depth
+    const int lds4 = sc.lds4;                       // <= kCurveLdsStack (rt_api.cpp): the column's allocated depth
     const uint32_t ovf_lane = blockIdx.x * 256u + threadIdx.x;
     const int scap = max(lds4, sc.stack4);          // commit_scene's bound on the walk's stack
     auto push = [&](const int32_t e) {
@@ -1791,16 +1851,22 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= RT_CURVE_FINISH_BATCH ||
                                              fin_m == __ballot(active));
         if (fin && flush) {
-            for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
-            if (best < 0) {
-                const v3 L = sky_radiance(sc, d);
-                if (depth0) {                                // throughput 1: (* 1 x) = x
-                    put_sample(rp, i, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
-                } else {
-                    const PathRec P = st.path[i];
-                    put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
+            if (gb + 1 < sc.n_groups || best < 0) {          // the groups after the BVH or the sky: the ray again
+                v3 o, d;
+                double tm;
+                ray_of(o, d, tm);
+                for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+                if (best < 0) {
+                    const v3 L = sky_radiance(sc, d);
+                    if (depth0) {                            // throughput 1: (* 1 x) = x
+                        put_sample(rp, i, 1.0 * L.x, 1.0 * L.y, 1.0 * L.z);
+                    } else {
+                        const PathRec P = st.path[i];
+                        put_sample(rp, P.wid, P.tr * L.x, P.tg * L.y, P.tb * L.z);
+                    }
                 }
-            } else {
+            }
+            if (best >= 0) {
                 hr = HitRec{closest, best, i};
                 cls = sc.leaf_cls[best];                     // a byte per leaf (1 MB at C5), not the 128-B record
             }
@@ -1825,22 +1891,21 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
                 if (kk < n) {
                     k = kk;
                     i = qphys(qm, kk);
-                    const RayRec R = st.ray[i];
-                    o = mk(R.ox, R.oy, R.oz);
-                    d = mk(R.dx, R.dy, R.dz);
-                    tm = depth0 ? st.tm[i] : 0.0;
+                    v3 o, d;
+                    double tm;
+                    ray_of(o, d, tm);
                     closest = kTmax;
                     best = -1;
-                    for (int g = 0; g < gb; ++g) group_closest<F>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
-                    a = dot(d, d);
-                    ia = 1.0 / a;
+                    for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
                     br = box_ray(o, d);
-                    tscale = fmax(1.0, 1.0 / sqrt(a));
+                    tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
                     bez_ray(o, d, W.ray[lane]);
                     W.done[lane] = 0u;
                     queued = 0u;
                     sp = 0; node = sc.bvh4_root; trav = gb < sc.n_groups; pb = pe = 0;
+#if RT_CURVE_PREFETCH
                     if (trav && node >= 0) N = sc.bvh4[node];
+#endif
                     active = true;
                     ray_it = 0;
                 }
@@ -1854,6 +1919,9 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
         //    nearest first, the nearest entered, the others pushed
         if (active && trav && pb >= pe) {
             if (node >= 0) {
+#if !RT_CURVE_PREFETCH
+                const BvhNode4 N = sc.bvh4[node];
+#endif
                 const float tcap = f32_up(closest * tscale);
                 float key[4];
                 int32_t ref[4];
@@ -1897,29 +1965,37 @@ __global__ __launch_bounds__(256, 2) void k_extend_curves(const DevScene sc, con
                 else node = pop();
             } else {
                 const BvhLeaf L = sc.bleaf[~node];
-                for (int s = L.sb; s < L.sb + L.sn; ++s) {
-                    const SphereRec S = sc.sph[s];
-                    sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
-                }
-                for (int s = L.mb; s < L.mb + L.mn; ++s) {
-                    const MSphereRec S = sc.msph[s];
-                    const double frac = (tm - S.t0) / S.den;
-                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                    sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
+                if (L.sn + L.mn > 0) {                              // spheres in the curve tree: the ray again
+                    v3 o, d;
+                    double tm;
+                    ray_of(o, d, tm);
+                    const double a = dot(d, d), ia = 1.0 / a;
+                    for (int s = L.sb; s < L.sb + L.sn; ++s) {
+                        const SphereRec S = sc.sph[s];
+                        sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
+                    }
+                    for (int s = L.mb; s < L.mb + L.mn; ++s) {
+                        const MSphereRec S = sc.msph[s];
+                        const double frac = (tm - S.t0) / S.den;
+                        const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
+                        sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
+                    }
                 }
                 pb = L.bb; pe = L.bb + L.bn;
                 if (sp == 0) trav = false;
                 else node = pop();
             }
         }
-        // the next node's record, in flight while the batches below run (+5 % at C5)
+#if RT_CURVE_PREFETCH
+        // the next node's record, in flight while the batches below run (+5 % at C5 with 2 waves per SIMD)
         if (active && trav && node >= 0) N = sc.bvh4[node];
+#endif
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk3 += t - st_t; st_t = t; }
 #endif
-        // 4. queue this step's curve candidates (at most 2 per lane)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        // 4. queue one of the lane's curve candidates (kBezQ: at most one per lane per step; a leaf with
+        //    several curves queues them over the next iterations, its traversal paused meanwhile)
+        {
             const bool has = active && pb < pe;
             const unsigned long long m = __ballot(has);
             if (has) { W.q[qn + lanes_below(m)] = ((uint32_t)pb << 6) | lane; ++pb; ++queued; }
@@ -2728,22 +2804,32 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
                          uint32_t* counts, bool depth0, unsigned int* claim, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
-    if (scene_features(sc) == kFeatCurves && sc.bvh_has_bez && claim && curve_blocks() > 0) {
-        // resident blocks only: later blocks would find the rays claimed
+    // the persistent curve kernel: every curve in the world BVH (its groups outside the BVH are spheres and
+    // rects only: group_closest<0>, so the per-lane curve walk is not compiled into it)
+    if (scene_features(sc) == kFeatCurves && sc.bvh_has_bez && sc.bez_groups == 0 && claim && curve_blocks() > 0) {
+        // resident blocks only: later blocks would find the rays claimed.  The BVH4 walk's LDS stack column
+        // holds lds4 entries per lane (the rest in the overflow area).  Occupancy per (device, LDS bytes)
+        const size_t clds = (size_t)256 * (size_t)(sc.lds4 > 0 ? sc.lds4 : 1) * sizeof(uint32_t);
+        static int occ_dev = -1;
         static size_t occ_lds = ~(size_t)0;
         static uint32_t occ_blocks = 0;
-        if (occ_lds != lds) {
-            int per_cu = 0, dev = 0, cus = 0;
-            HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_curves, 256, lds));
-            HIP_RETURN_IF(hipGetDevice(&dev));
+        int dev = 0;
+        HIP_RETURN_IF(hipGetDevice(&dev));
+        if (occ_lds != clds || occ_dev != dev) {
+            int per_cu = 0, cus = 0;
+            HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend_curves, 256, clds));
             HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             occ_blocks = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
-            occ_lds = lds;
+            occ_lds = clds;
+            occ_dev = dev;
         }
         uint32_t pb = blocks < occ_blocks ? blocks : occ_blocks;
         if (pb > curve_blocks()) pb = curve_blocks();
+        // the overflow area holds sc.ovf_lanes lanes per render lane: never launch more (ovf_lane indexes it)
+        if (sc.stk_ovf && pb > sc.ovf_lanes / 256u) pb = sc.ovf_lanes / 256u;
+        if (pb == 0u) pb = 1u;
         HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-        hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), lds, s, sc, rp, st, in, n, hit,
+        hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
                            shard_cap, counts, depth0, claim);
         return hipGetLastError();
     }

@@ -45,6 +45,7 @@ def main():
         "kernel_clock_per_iter": b[40] / max(1, b[23]),
         "step1_finish_share": b[42] / max(1, b[40]), "step2_claim_share": b[43] / max(1, b[40]),
         "step3_bvh_share": b[44] / max(1, b[40]), "stage_b_refill_share": b[45] / max(1, b[40]),
+        "stage_b_leaf_share": b[46] / max(1, b[40]), "stage_b_node_share": b[47] / max(1, b[40]),
     }
     print(json.dumps(out, indent=1))
 
