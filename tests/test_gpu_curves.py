@@ -150,10 +150,13 @@ def test_curve_deeper_than_walk_faults(sched, wavefront):
 
 def test_duplicate_curves_tie_to_the_later_curve(sched, oracle_mod):
     """Curves duplicated exactly (same control points, other materials) in a
-    BVH: every tie in z must go to the later curve of the list, as
+    BVH: every tie in z goes to the later curve of the list, as a flat
     hit-obj-list's scan keeps a curve at z <= t-max (geometry.scm:41-46,
-    bezier.scm:164).  rt_hit_rays against the oracle's hit_world, material by
-    material; the render against the oracle too."""
+    bezier.scm:164).  This is the project's convention for BVHs, shared by the
+    oracle: the reference's own BVH breaks ties by tree shape
+    (geometry.scm:252-254, 360-365, a random split axis), and no reference
+    output covers exact ties.  rt_hit_rays against the oracle's hit_world,
+    material by material; the render against the oracle too."""
     rs = np.random.default_rng(0x5EED0106)
     mats = [g.make_lambertian(g.constant_texture(v.vec3(0.2 + 0.2 * k, 0.5, 0.3))) for k in range(3)]
     cps = rs.uniform(100.0, 450.0, size=(300, 12))
