@@ -92,9 +92,6 @@ struct DevBuf {
 // overlaps the wide first iterations of the next one instead of leaving the
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
 constexpr int kLanes = 4;                  // most lanes a render may use (RT_OPT_LANES)
-#ifndef RT_CURVE_LDS_STACK
-#define RT_CURVE_LDS_STACK 8
-#endif
 constexpr int kCurveLdsStack = RT_CURVE_LDS_STACK;   // k_extend_curves' BVH4 stack entries in LDS per lane
 struct Lane {
     DevBuf st_a, st_b, hit, sb, counts, seg_tail;

@@ -126,6 +126,14 @@ struct DevCamera {            // camera.scm:33-78 (the 10 slots)
     double lens, t0, t1;
 };
 
+// k_extend_curves' BVH4 stack entries per lane in LDS (the rest of a deep walk's stack goes to the
+// overflow area).  15 is the most that keeps two 256-thread blocks (the register-bound occupancy) on a
+// 160-KiB CU beside the blocks' BezWave state; C5 at 8 spp: 8 -> 320, 12 -> 337, 15 -> 340 Mrays/s
+// (profiles/r04/ab_stack.log)
+#ifndef RT_CURVE_LDS_STACK
+#define RT_CURVE_LDS_STACK 15
+#endif
+
 struct DevScene {
     const SphereRec* sph;  int32_t n_sph;
     const MSphereRec* msph; int32_t n_msph;

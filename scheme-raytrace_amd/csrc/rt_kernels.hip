@@ -335,7 +335,6 @@ __device__ __forceinline__ v3 bez_tan(const Bez4& c, const bool one) {         /
 }
 __device__ __forceinline__ double dot2d(const v3 a, const v3 b) { return (a.x * b.x + a.y * b.y) + 0.0 * 0.0; }
 
-
 __device__ __forceinline__ void bez_load(const BezierRec& B, const BezRay& R, Bez4& c) {   // bezier-transform :99-105
     c.p0 = bez_xf(R, B.cp[0], B.cp[1], B.cp[2]);
     c.p1 = bez_xf(R, B.cp[3], B.cp[4], B.cp[5]);
@@ -657,6 +656,9 @@ constexpr int kBezRefill = RT_BEZ_REFILL;   // stage B: idle lanes that take the
 #ifndef RT_BEZ_WAIT_FLUSH
 #define RT_BEZ_WAIT_FLUSH 0            // k_extend_curves: lanes waiting on their curves that force a batch (0 = off)
 #endif
+#ifndef RT_BEZ_SLOT
+#define RT_BEZ_SLOT 1                  // stage B: an LDS slot per lane for its latest pending right sibling
+#endif
 #ifndef RT_BEZ_QFLUSH
 #define RT_BEZ_QFLUSH 48               // k_extend_curves: queued candidates that trigger a batch (stage A)
 #endif
@@ -682,7 +684,9 @@ struct BezWave {
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
     uint32_t done[64];              // persistent kernel: owner's candidates resolved so far
+#if RT_BEZ_SLOT
     Bez4 pend[64];                  // stage B: each lane's latest pending right sibling (bez_walk_split)
+#endif
     uint8_t lev[kBezS];             // survivors' subdivision leaf levels (stage A)
 };
 __device__ __forceinline__ void wave_sync() {
@@ -847,7 +851,11 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             const unsigned long long cl1 = __builtin_amdgcn_s_memtime();
             n_clk_leaf += cl1 - cl0;
 #endif
+#if RT_BEZ_SLOT
             if (busy && !at_leaf) over = bez_walk_node<true>(wk, &W.pend[threadIdx.x & 63u]);
+#else
+            if (busy && !at_leaf) over = bez_walk_node(wk);
+#endif
 #ifdef RT_STATS
             n_clk_node += __builtin_amdgcn_s_memtime() - cl1;
 #endif
@@ -1761,6 +1769,8 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 #ifndef RT_CURVE_WAVES
 #define RT_CURVE_WAVES 2               // waves per SIMD k_extend_curves is compiled for (VGPR budget 512 / waves)
 #endif
+static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK <= 160 * 1024 / RT_CURVE_WAVES,
+              "k_extend_curves: RT_CURVE_WAVES blocks of BezWave state and LDS stack columns must fit a CU's LDS");
 #ifndef RT_CURVE_PREFETCH
 #define RT_CURVE_PREFETCH 1            // load the lane's next BVH4 node one iteration ahead (32 VGPRs)
 #endif
@@ -1785,6 +1795,9 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
     // B's walk state fits beside the loop's (registers cap the waves per SIMD, RT_CURVE_WAVES)
     double tscale = 1.0, closest = kTmax;
     int32_t best = -1, node = 0;
+    // best's material class (leaf_cls), loaded whenever best changes: the load is in flight while the
+    // traversal goes on, not a round trip of the finish
+    int32_t bcls = -1;
     BoxRay br{};
 #if RT_CURVE_PREFETCH
     BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
@@ -1856,6 +1869,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                 double tm;
                 ray_of(o, d, tm);
                 for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+                if (gb + 1 < sc.n_groups && best >= 0) bcls = sc.leaf_cls[best];
                 if (best < 0) {
                     const v3 L = sky_radiance(sc, d);
                     if (depth0) {                            // throughput 1: (* 1 x) = x
@@ -1868,7 +1882,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
             }
             if (best >= 0) {
                 hr = HitRec{closest, best, i};
-                cls = sc.leaf_cls[best];                     // a byte per leaf (1 MB at C5), not the 128-B record
+                cls = bcls;                                  // a byte per leaf (1 MB at C5), not the 128-B record
             }
             active = false;
         }
@@ -1897,6 +1911,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                     closest = kTmax;
                     best = -1;
                     for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+                    bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
                     br = box_ray(o, d);
                     tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
                     bez_ray(o, d, W.ray[lane]);
@@ -1980,6 +1995,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                         const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
                         sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
                     }
+                    bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
                 }
                 pb = L.bb; pe = L.bb + L.bn;
                 if (sp == 0) trav = false;
@@ -2030,7 +2046,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                 wave_sync();
                 bez_stage_b<true>(sc, W, nb, svn);
                 svn -= nb;
-                if (active) bez_take_batch(sc, W, lane, bz, closest, best);
+                if (active) {
+                    const int32_t b0 = best;
+                    bez_take_batch(sc, W, lane, bz, closest, best);
+                    if (best != b0) bcls = sc.leaf_cls[best];
+                }
                 wave_sync();
             }
         }
