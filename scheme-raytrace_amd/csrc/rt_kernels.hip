@@ -381,17 +381,25 @@ __device__ __forceinline__ bool bez_sep_axis(const Bez4& c, const v3 a, const v3
 // straight); 4: the chord and the three legs of the control polygon (roots;
 // the two diagonals as well cut C5's survivors by another ~10 % in a host
 // simulation but cost more in stage A than they save: -1.2 % at 8 spp)
-template <int EDGES>
-__device__ __forceinline__ bool bez_hull_culled(const Bez4& c, const double w1) {
-    if (!RT_BEZ_HULL) return false;
+// r^2 for the control points c; a sub-curve's points are convex combinations of its root's (a few ulps
+// aside), so the root's r bounds every node's and the walk computes it once (BezWalk::hr2)
+__device__ __forceinline__ double bez_hull_r2(const Bez4& c, const double w1) {
     const double s = fmax(fmax(fmax(fabs(c.p0.x), fabs(c.p0.y)), fmax(fabs(c.p1.x), fabs(c.p1.y))),
                           fmax(fmax(fabs(c.p2.x), fabs(c.p2.y)), fmax(fabs(c.p3.x), fabs(c.p3.y))));
     const double r = fma(w1, 1e-9, w1) + 1e-9 * s;
-    const double r2 = r * r;
+    return r * r;
+}
+template <int EDGES>
+__device__ __forceinline__ bool bez_hull_sep(const Bez4& c, const double r2) {
+    if (!RT_BEZ_HULL) return false;
     bool sep = bez_sep_axis(c, c.p0, c.p3, r2);
     if (EDGES > 1)
         sep = sep || bez_sep_axis(c, c.p0, c.p1, r2) || bez_sep_axis(c, c.p1, c.p2, r2) || bez_sep_axis(c, c.p2, c.p3, r2);
     return sep;
+}
+template <int EDGES>
+__device__ __forceinline__ bool bez_hull_culled(const Bez4& c, const double w1) {
+    return RT_BEZ_HULL && bez_hull_sep<EDGES>(c, bez_hull_r2(c, w1));
 }
 // converge's box cull plus the hull cull
 template <int EDGES>
@@ -433,6 +441,7 @@ __device__ __forceinline__ bool bez_culled_hull(const Bez4& c, const double w1, 
 struct BezWalk {
     Bez4 root, c;
     double best, tmax, w1, w2;
+    double hr2;                     // the hull cull's r^2 from the root (bez_hull_r2)
     int L, leaf_level, base;        // base: the level the walk started at (a donated subtree's root; else 0)
     int rl;                         // re-derivation (!fresh): c is the path node at level rl < L
     uint32_t idx, it, cap;
@@ -458,6 +467,7 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
                                               const double tmax, const int leaf_level) {
     s.root = root; s.c = root;
     s.w1 = w1; s.w2 = w2; s.tmax = tmax;
+    s.hr2 = bez_hull_r2(root, w1);
     s.leaf_level = leaf_level;
     // each of the <= 2^(leaf_level+1) nodes is visited at most once, for at
     // most leaf_level re-derivation splits and one split or leaf test
@@ -505,7 +515,8 @@ __device__ __forceinline__ bool bez_walk_split(BezWalk& s, Bez4* slot = nullptr)
         return bez_walk_next(s);                                // (its hull passed at its first split)
     }
     // (:123-128) with the best z so far
-    const bool kl = !bez_culled_hull<1>(l, s.w1, s.best), kr = !bez_culled_hull<1>(r, s.w1, s.best);
+    const bool kl = !(bez_culled(l, s.w1, s.best) || bez_hull_sep<1>(l, s.hr2));
+    const bool kr = !(bez_culled(r, s.w1, s.best) || bez_hull_sep<1>(r, s.hr2));
     if (kl || kr) {
         ++s.L;
         if (kl) {
