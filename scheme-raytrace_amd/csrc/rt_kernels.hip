@@ -1974,9 +1974,19 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                     if (sp == 0) trav = false;
                     else node = pop();
                 } else {
-                    if (key[3] != INFINITY) push(ref[3]);
-                    if (key[2] != INFINITY) push(ref[2]);
-                    if (key[1] != INFINITY) push(ref[1]);
+                    // the hit children beyond the nearest, farthest first (the keys are sorted, misses last)
+                    const int np = (key[1] != INFINITY) + (key[2] != INFINITY) + (key[3] != INFINITY);
+                    if (sp + np <= lds4) {                      // all in the LDS column: no per-push branches
+                        uint32_t* top = lstk + sp * stride;
+                        if (np >= 3) { top[0] = (uint32_t)ref[3]; top += stride; }
+                        if (np >= 2) { top[0] = (uint32_t)ref[2]; top += stride; }
+                        if (np >= 1) top[0] = (uint32_t)ref[1];
+                        sp += np;
+                    } else {
+                        if (key[3] != INFINITY) push(ref[3]);
+                        if (key[2] != INFINITY) push(ref[2]);
+                        if (key[1] != INFINITY) push(ref[1]);
+                    }
                     node = ref[0];
                 }
                 // a leaf holding one curve: queued from its ref in this step (no leaf record, no extra step)
