@@ -156,7 +156,7 @@ struct Scene {
     DevScene dev{};
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
-    DevBuf d_bvh4, d_stk_ovf;                      // curve trees: BVH4 and the walk's stack overflow
+    DevBuf d_bvh4, d_stk_ovf, d_bez_ring;                      // curve trees: BVH4 and the walk's stack overflow
     DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
     DevBuf d_leaf_cls;
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
@@ -1030,6 +1030,14 @@ int commit_scene(Scene* s, int world) {
         // entries, so the walk exercises its overflow area
         const char* ce = std::getenv("RTAMD_CURVE_LDS_STACK");
         d.lds4 = std::min(lane_stack, ce ? std::max(1, std::atoi(ce)) : kCurveLdsStack);
+        {                                            // survivor rings: two 256-thread blocks per CU
+            int dev = 0, cus = 0;
+            HIPCHK(hipGetDevice(&dev));
+            HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            d.ring_waves = (uint32_t)std::max(cus, 1) * 8u;
+            HIPCHK(s->d_bez_ring.ensure((size_t)kLanes * d.ring_waves * kBezRing * 128u));
+            d.bez_ring = s->d_bez_ring.as<double>();
+        }
         if (stack4 > d.lds4) {                       // the walk's deepest stacks spill past the LDS columns
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
@@ -1366,6 +1374,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             // the curve walk's stack overflow area: one region per render lane (lanes run concurrently)
             DevScene dl = s->dev;
             if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lds4);
+            if (dl.bez_ring) dl.bez_ring += (size_t)L.index * dl.ring_waves * kBezRing * 16u;
             HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
                                  reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1), L.stream));

@@ -130,6 +130,7 @@ struct DevCamera {            // camera.scm:33-78 (the 10 slots)
 // overflow area).  15 is the most that keeps two 256-thread blocks (the register-bound occupancy) on a
 // 160-KiB CU beside the blocks' BezWave state; C5 at 8 spp: 8 -> 320, 12 -> 337, 15 -> 340 Mrays/s
 // (profiles/r04/ab_stack.log)
+constexpr int kBezRing = 256;                  // survivor ring entries per wave (> the survivors a wave holds)
 #ifndef RT_CURVE_LDS_STACK
 #define RT_CURVE_LDS_STACK 15
 #endif
@@ -154,6 +155,9 @@ struct DevScene {
     // words per lane of a grid of at most ovf_lanes lanes (entry e of lane g at e * lanes + g);
     // the buffer holds one such region per render lane and each launch gets its lane's (rt_api.cpp)
     const BvhNode4* bvh4;  int32_t n_bvh4;
+    // k_extend_curves' survivor rings: per resident wave kBezRing entries of 128 B (a root-culled curve's
+    // ray-space control points and widths, written by stage A, read by stage B's refills and takes)
+    double* bez_ring;  uint32_t ring_waves;
     int32_t bvh4_root, stack4;
     int32_t lds4;                                  // the walk's stack entries in LDS (lane_stack; tests lower it)
     uint32_t* stk_ovf;     uint32_t ovf_lanes;

@@ -603,6 +603,24 @@ __device__ __forceinline__ void bez_walk_donate(BezWalk& s, const uint32_t pend,
     s.rmask |= 1u << l;
     if (s.pl == (int)l) s.pl = -1;                              // it is not this walk's any more
 }
+// A root-culled curve as stage A leaves it for stage B (k_extend_curves' survivor ring): the
+// ray-space control points and the widths, so a refill reads 128 B the wave wrote itself (an L2 hit)
+// instead of the curve record and the owner's matrix, and does not transform again
+struct alignas(16) BezRoot { Bez4 c; double w1, w2, pad0, pad1; };
+static_assert(sizeof(BezRoot) == 128, "BezRoot is one 128-B line");
+__device__ __forceinline__ bool bez_walk_begin_root(BezWalk& s, const BezRoot& R, const double tmax,
+                                                    const int leaf_level) {
+    const Bez4 root = R.c;
+    const double w1 = R.w1, w2 = R.w2;
+    if (bez_culled(root, w1, tmax)) return false;
+    bez_walk_init(s, root, w1, w2, tmax, leaf_level);
+    return true;
+}
+__device__ __forceinline__ void bez_walk_take_root(BezWalk& s, const BezRoot& R, const double tmax,
+                                                   const int leaf_level, const uint32_t l, const uint32_t ridx) {
+    bez_walk_init(s, R.c, R.w1, R.w2, tmax, leaf_level);
+    s.L = (int)l; s.base = (int)l; s.idx = ridx; s.fresh = false;
+}
 // Start a walk of the donated subtree rooted at node (l, ridx) of curve B
 // (re-derived from the root at the first step; the walk ends back at level l).
 __device__ __forceinline__ void bez_walk_take(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
@@ -711,8 +729,10 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 // Stage A: root cull of the qn queued candidates; survivors are appended to
 // the survivor list (svn entries already there).  Returns the new count.
 // Every active lane calls it with the same arguments.
+// TRACK (k_extend_curves): survivors also go to the wave's ring (slot rtail + position, mod kBezRing)
 template <bool TRACK = false>
-__device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, const uint32_t qn, uint32_t svn) {
+__device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, const uint32_t qn, uint32_t svn,
+                                                BezRoot* __restrict__ ring = nullptr, const uint32_t rtail = 0u) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
     for (uint32_t base = 0; base < qn; base += nact) {
@@ -720,10 +740,10 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
         bool keep = false;
         uint32_t e = 0;
         uint8_t lev = 0;
+        Bez4 c;
         if (i < qn) {
             e = W.q[i];
             const BezierRec& B = sc.bez[e >> 6];
-            Bez4 c;
             bez_load(B, W.ray[e & 63u], c);
             keep = !bez_culled_hull<4>(c, B.w1, W.cl[e & 63u]);
             // leaf level maxd + 1, at least 0: a flat curve's maxd is negative (its root is a leaf);
@@ -736,7 +756,14 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
             if (TRACK && !keep) atomicAdd(&W.done[e & 63u], 1u);
         }
         const unsigned long long m = __ballot(keep);
-        if (keep) { W.sv[svn + lanes_below(m)] = e; W.lev[svn + lanes_below(m)] = lev; }
+        if (keep) {
+            const uint32_t pos = svn + lanes_below(m);
+            W.sv[pos] = e; W.lev[pos] = lev;
+            if (TRACK) {
+                const BezierRec& B = sc.bez[e >> 6];
+                ring[(rtail + pos) & (uint32_t)(kBezRing - 1)] = BezRoot{c, B.w1, B.w2, 0.0, 0.0};
+            }
+        }
         svn += (uint32_t)__popcll(m);
 #ifdef RT_STATS
         if (rank == 0) RT_STAT(15, __popcll(m));
@@ -756,7 +783,8 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
 // read and cleared by take_curve_stats.
 __device__ unsigned long long g_curve_stats[2];
 template <bool TRACK = false>
-__device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn) {
+__device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn,
+                                            const BezRoot* __restrict__ ring = nullptr, const uint32_t rtail = 0u) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
     if (nb >= (uint32_t)RT_BEZ_HOLD) {
@@ -811,7 +839,8 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                         const uint32_t e = W.sv[i];
                         si = i;
                         W.sz[i] = INFINITY;
-                        busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
+                        busy = TRACK ? bez_walk_begin_root(wk, ring[(rtail + i) & (uint32_t)(kBezRing - 1)], W.cl[e & 63u], W.lev[i])
+                                     : bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
@@ -832,8 +861,12 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (!busy && ir < nd) {
                         si = W.q[2 * ir];
                         const uint32_t e = W.sv[si], lr = W.q[2 * ir + 1];
-                        bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], lr >> 26,
-                                      lr & ((1u << 26) - 1u));
+                        if (TRACK)
+                            bez_walk_take_root(wk, ring[(rtail + si) & (uint32_t)(kBezRing - 1)], W.cl[e & 63u], W.lev[si],
+                                               lr >> 26, lr & ((1u << 26) - 1u));
+                        else
+                            bez_walk_take(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[si], lr >> 26,
+                                          lr & ((1u << 26) - 1u));
                         busy = true;
                     }
                     wave_sync();
@@ -1835,6 +1868,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
         return (int32_t)(sp < lds4 ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lds4) * sc.ovf_lanes + ovf_lane]);
     };
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
+    // the wave's survivor ring (launch_extend_curves keeps the grid within sc.ring_waves) and the ring
+    // slot of survivor 0: survivors are taken oldest first, so slot = rtail + position
+    BezRoot* const ring = reinterpret_cast<BezRoot*>(sc.bez_ring) +
+                          (size_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * (size_t)kBezRing;
+    uint32_t rtail = 0;
     // a ray takes at most one step per node / leaf and one queue step per two curves: bound its
     // working iterations (a valid walk stays far below)
     const uint32_t ray_cap = g_curve_ray_cap ? g_curve_ray_cap : 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
@@ -2055,7 +2093,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
 #ifdef RT_STATS
             const unsigned long long ca = __builtin_amdgcn_s_memtime();
 #endif
-            svn = bez_stage_a<true>(sc, W, qn, svn);
+            svn = bez_stage_a<true>(sc, W, qn, svn, ring, rtail);
 #ifdef RT_STATS
             st_clk_a += __builtin_amdgcn_s_memtime() - ca;
 #endif
@@ -2065,8 +2103,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                 W.hz[lane] = INFINITY;
                 W.hkey[lane] = 0ull;
                 wave_sync();
-                bez_stage_b<true>(sc, W, nb, svn);
+                // the ring entries other lanes wrote: stores complete and visible to the wave's loads
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                bez_stage_b<true>(sc, W, nb, svn, ring, rtail);
                 svn -= nb;
+                rtail += nb;
                 if (active) {
                     const int32_t b0 = best;
                     bez_take_batch(sc, W, lane, bz, closest, best);
@@ -2868,6 +2909,7 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
         if (pb > curve_blocks()) pb = curve_blocks();
         // the overflow area holds sc.ovf_lanes lanes per render lane: never launch more (ovf_lane indexes it)
         if (sc.stk_ovf && pb > sc.ovf_lanes / 256u) pb = sc.ovf_lanes / 256u;
+        if (pb > sc.ring_waves / 4u) pb = sc.ring_waves / 4u;   // one survivor ring per wave
         if (pb == 0u) pb = 1u;
         HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
         hipLaunchKernelGGL(k_extend_curves, dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
