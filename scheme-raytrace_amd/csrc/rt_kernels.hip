@@ -702,6 +702,8 @@ constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 64;   // < the
 #define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
 #endif
 constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
+static_assert(kBezS <= kBezRing && (kBezRing & (kBezRing - 1)) == 0,
+              "k_extend_curves' survivor ring holds every survivor a wave can hold (slot = rtail + position)");
 static_assert(2 * 64 <= kBezQ, "stage B's donation handover: two words per donor lane in W.q");
 static_assert(kBezMaxDepth + 1 < 26, "the handover packs a level (6 bits) above a node index (26 bits)");
 struct BezWave {
