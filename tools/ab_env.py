@@ -27,7 +27,7 @@ def main():
     p.add_argument("--spp", type=int, default=256)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--lanes", default=None, help="render lanes (RT_OPT_LANES) for every variant")
-    p.add_argument("variants", nargs="+", help="name:ENV=V,ENV2=V2 (name: alone = defaults)")
+    p.add_argument("variants", nargs="+", help="name:ENV=V,opt.tail_div=256 (name: alone = defaults)")
     a = p.parse_args()
     import torch
     from rtamd import gpu, scenes
@@ -44,11 +44,20 @@ def main():
     acc = torch.zeros(a.nx * a.ny * 3, dtype=torch.float64, device="cuda")
 
     def with_env(env, fn):
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        # keys "opt.<name>" are context options (rt_context_set_option), the rest environment variables
+        opts = {k[4:]: int(v) for k, v in env.items() if k.startswith("opt.")}
+        envs = {k: v for k, v in env.items() if not k.startswith("opt.")}
+        old = {k: os.environ.get(k) for k in envs}
+        os.environ.update(envs)
+        for k, v in opts.items():
+            ctx.set_option(k, v)
         try:
             return fn()
         finally:
+            for k in opts:
+                ctx.set_option(k, 0)
+            if a.lanes:
+                ctx.set_option("lanes", int(a.lanes))
             for k, v in old.items():
                 if v is None:
                     os.environ.pop(k, None)
