@@ -1030,11 +1030,11 @@ int commit_scene(Scene* s, int world) {
         // entries, so the walk exercises its overflow area
         const char* ce = std::getenv("RTAMD_CURVE_LDS_STACK");
         d.lds4 = std::min(lane_stack, ce ? std::max(1, std::atoi(ce)) : kCurveLdsStack);
-        {                                            // survivor rings: two 256-thread blocks per CU
+        {                                            // survivor rings: RT_CURVE_WAVES 256-thread blocks per CU
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
             HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            d.ring_waves = (uint32_t)std::max(cus, 1) * 8u;
+            d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * RT_CURVE_WAVES;
             HIPCHK(s->d_bez_ring.ensure((size_t)kLanes * d.ring_waves * kBezRing * 128u));
             d.bez_ring = s->d_bez_ring.as<double>();
         }

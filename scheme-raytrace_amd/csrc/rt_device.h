@@ -131,6 +131,9 @@ struct DevCamera {            // camera.scm:33-78 (the 10 slots)
 // 160-KiB CU beside the blocks' BezWave state; C5 at 8 spp: 8 -> 320, 12 -> 337, 15 -> 340 Mrays/s
 // (profiles/r04/ab_stack.log)
 constexpr int kBezRing = 256;                  // survivor ring entries per wave (> the survivors a wave holds)
+#ifndef RT_CURVE_WAVES
+#define RT_CURVE_WAVES 2               // waves per SIMD k_extend_curves is compiled for (VGPR budget 512 / waves)
+#endif
 #ifndef RT_CURVE_LDS_STACK
 #define RT_CURVE_LDS_STACK 15
 #endif

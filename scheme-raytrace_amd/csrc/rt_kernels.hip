@@ -438,8 +438,13 @@ __device__ __forceinline__ bool bez_culled_hull(const Bez4& c, const double w1, 
 // and bez_walk_leaf (a leaf segment's test).  Stage B calls node / leaf, and
 // holds lanes at leaf segments until enough of them test together
 // (RT_BEZ_LEAF_PHASE); the per-lane bezier_test calls split / leaf.
-struct BezWalk {
-    Bez4 root, c;
+// RING (k_extend_curves' stage B): the root is not held in registers — the walk re-reads it from the
+// survivor's ring line when it re-derives a node (24 VGPRs less at the kernel's peak)
+template <bool RING> struct BezRootOf { Bez4 root; };
+template <> struct BezRootOf<true> { const Bez4* rootp; };
+template <bool RING = false>
+struct BezWalkT : BezRootOf<RING> {
+    Bez4 c;
     double best, tmax, w1, w2;
     double hr2;                     // the hull cull's r^2 from the root (bez_hull_r2)
     int L, leaf_level, base;        // base: the level the walk started at (a donated subtree's root; else 0)
@@ -449,6 +454,12 @@ struct BezWalk {
     int pl;                         // the level of the pending right sibling held in the lane's LDS slot (-1: none)
     bool fresh, found;              // fresh: c is node (L, idx) and passed the cull
 };
+using BezWalk = BezWalkT<false>;
+template <bool RING>
+__device__ __forceinline__ Bez4 bez_root(const BezWalkT<RING>& s) {
+    if constexpr (RING) return *s.rootp;
+    else return s.root;
+}
 // converge's subdivision depth from the transformed curve's flatness (:180-193)
 __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
     double l0 = -kTmax;
@@ -463,9 +474,12 @@ __device__ __forceinline__ int bez_maxd(const Bez4& c, const double eps8) {
 // set up the walk of root-transformed curve `root` for t-max tmax (the root
 // has passed the cull) down to leaf level leaf_level = max(0, maxd + 1): a
 // negative maxd (a flat curve) makes the root a leaf (:130, 189-193)
-__device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, const double w1, const double w2,
-                                              const double tmax, const int leaf_level) {
-    s.root = root; s.c = root;
+template <bool RING>
+__device__ __forceinline__ void bez_walk_init(BezWalkT<RING>& s, const Bez4& root, const double w1, const double w2,
+                                              const double tmax, const int leaf_level, const Bez4* rootp = nullptr) {
+    if constexpr (RING) s.rootp = rootp;
+    else s.root = root;
+    s.c = root;
     s.w1 = w1; s.w2 = w2; s.tmax = tmax;
     s.hr2 = bez_hull_r2(root, w1);
     s.leaf_level = leaf_level;
@@ -476,7 +490,8 @@ __device__ __forceinline__ void bez_walk_init(BezWalk& s, const Bez4& root, cons
     s.fresh = true; s.found = false; s.best = tmax;
 }
 // at a leaf segment: the next call is bez_walk_leaf
-__device__ __forceinline__ bool bez_walk_at_leaf(const BezWalk& s) { return s.fresh && s.L >= s.leaf_level; }
+template <bool RING>
+__device__ __forceinline__ bool bez_walk_at_leaf(const BezWalkT<RING>& s) { return s.fresh && s.L >= s.leaf_level; }
 // set up the walk of curve B for t-max tmax, whose leaf level (maxd + 1, from
 // stage A's root cull) is given; false if the whole curve is culled
 __device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, const BezRay& R, const double tmax,
@@ -490,11 +505,13 @@ __device__ __forceinline__ bool bez_walk_begin(BezWalk& s, const BezierRec& B, c
 // past the current node: climb past right halves and past left halves whose
 // right sibling was culled at the split, then aim at the surviving right
 // sibling (re-derived from the root); true once the walk is over
-__device__ __forceinline__ bool bez_walk_next(BezWalk& s) {
+template <bool RING>
+__device__ __forceinline__ bool bez_walk_next(BezWalkT<RING>& s) {
     while (s.L > s.base && ((s.idx & 1u) || ((s.rmask >> s.L) & 1u))) { --s.L; s.idx >>= 1; }
     if (s.L == s.base) return true;
     ++s.idx;
-    s.c = s.root; s.rl = 0; s.fresh = false;
+    if constexpr (!RING) s.c = s.root;              // (RING walks re-derive in bez_walk_node only)
+    s.rl = 0; s.fresh = false;
     return false;
 }
 // one split (not at a leaf: !bez_walk_at_leaf); true once the walk is over
@@ -502,8 +519,8 @@ __device__ __forceinline__ bool bez_walk_next(BezWalk& s) {
 // sibling.  Depth first, that sibling is the next pending node the walk turns to (every later one lies in
 // its left brother's subtree and is visited first), so the walk takes it from the slot instead of
 // re-deriving it from the root, bit for bit the same values; older ones are overwritten and re-derived.
-template <bool SLOT = false>
-__device__ __forceinline__ bool bez_walk_split(BezWalk& s, Bez4* slot = nullptr) {
+template <bool SLOT = false, bool RING = false>
+__device__ __forceinline__ bool bez_walk_split(BezWalkT<RING>& s, Bez4* slot = nullptr) {
     if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
     Bez4 l, r;
     bez_split(s.c, l, r);                                       // split, left first (:167-175)
@@ -532,15 +549,15 @@ __device__ __forceinline__ bool bez_walk_split(BezWalk& s, Bez4* slot = nullptr)
 }
 // one node (not at a leaf): a pending right sibling is re-derived from the
 // root in one go, then split; true once the walk is over
-template <bool SLOT = false>
-__device__ __forceinline__ bool bez_walk_node(BezWalk& s, Bez4* slot = nullptr) {
+template <bool SLOT = false, bool RING = false>
+__device__ __forceinline__ bool bez_walk_node(BezWalkT<RING>& s, Bez4* slot = nullptr) {
     if (!s.fresh) {
         if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
         if (SLOT && s.pl == s.L) {                              // the pending sibling kept in the slot
             s.c = *slot;
             s.pl = -1;
         } else {
-            s.c = s.root;
+            s.c = bez_root(s);
             for (int k = s.L - 1; k >= 0; --k) {
                 Bez4 l, r;
                 bez_split(s.c, l, r);
@@ -555,7 +572,8 @@ __device__ __forceinline__ bool bez_walk_node(BezWalk& s, Bez4* slot = nullptr) 
     return bez_walk_split<SLOT>(s, slot);
 }
 // the leaf segment's test (:130-166) (bez_walk_at_leaf); true once the walk is over
-__device__ __forceinline__ bool bez_walk_leaf(BezWalk& s) {
+template <bool RING>
+__device__ __forceinline__ bool bez_walk_leaf(BezWalkT<RING>& s) {
     if (++s.it > s.cap + 1u) { raise_fault(RT_FAULT_CURVE); return true; }
     const Bez4& c = s.c;
     const double v0 = ldexp((double)s.idx, -s.L), vn = v0 + ldexp(1.0, -s.L);
@@ -589,7 +607,8 @@ __device__ __forceinline__ bool bez_walk_step(BezWalk& s) {
 // Work sharing: the right siblings still pending on a walk's path (levels
 // base+1 .. L whose path node is a left half whose right sibling survived its
 // split), as a bit mask by level.
-__device__ __forceinline__ uint32_t bez_walk_pending(const BezWalk& s) {
+template <bool RING>
+__device__ __forceinline__ uint32_t bez_walk_pending(const BezWalkT<RING>& s) {
     // level l's path node is a left half iff bit L - l of idx is 0: bit-reverse the complement so that
     // bit becomes bit l, keep levels base+1 .. L, drop the siblings culled at their split
     const uint32_t left = __builtin_bitreverse32(~s.idx & ((1u << s.L) - 1u)) >> (31 - s.L);
@@ -597,7 +616,8 @@ __device__ __forceinline__ uint32_t bez_walk_pending(const BezWalk& s) {
 }
 // Hand the shallowest pending right sibling to another lane: returns its
 // (level, index); this walk will skip it.
-__device__ __forceinline__ void bez_walk_donate(BezWalk& s, const uint32_t pend, uint32_t& l, uint32_t& ridx) {
+template <bool RING>
+__device__ __forceinline__ void bez_walk_donate(BezWalkT<RING>& s, const uint32_t pend, uint32_t& l, uint32_t& ridx) {
     l = (uint32_t)__builtin_ctz(pend);
     ridx = (s.idx >> ((uint32_t)s.L - l)) | 1u;
     s.rmask |= 1u << l;
@@ -608,17 +628,17 @@ __device__ __forceinline__ void bez_walk_donate(BezWalk& s, const uint32_t pend,
 // instead of the curve record and the owner's matrix, and does not transform again
 struct alignas(16) BezRoot { Bez4 c; double w1, w2, pad0, pad1; };
 static_assert(sizeof(BezRoot) == 128, "BezRoot is one 128-B line");
-__device__ __forceinline__ bool bez_walk_begin_root(BezWalk& s, const BezRoot& R, const double tmax,
+__device__ __forceinline__ bool bez_walk_begin_root(BezWalkT<true>& s, const BezRoot& R, const double tmax,
                                                     const int leaf_level) {
     const Bez4 root = R.c;
     const double w1 = R.w1, w2 = R.w2;
     if (bez_culled(root, w1, tmax)) return false;
-    bez_walk_init(s, root, w1, w2, tmax, leaf_level);
+    bez_walk_init(s, root, w1, w2, tmax, leaf_level, &R.c);
     return true;
 }
-__device__ __forceinline__ void bez_walk_take_root(BezWalk& s, const BezRoot& R, const double tmax,
+__device__ __forceinline__ void bez_walk_take_root(BezWalkT<true>& s, const BezRoot& R, const double tmax,
                                                    const int leaf_level, const uint32_t l, const uint32_t ridx) {
-    bez_walk_init(s, R.c, R.w1, R.w2, tmax, leaf_level);
+    bez_walk_init(s, R.c, R.w1, R.w2, tmax, leaf_level, &R.c);
     s.L = (int)l; s.base = (int)l; s.idx = ridx; s.fresh = false;
 }
 // Start a walk of the donated subtree rooted at node (l, ridx) of curve B
@@ -807,7 +827,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
     // that walked part of it (atomicMin on the bits of the positive doubles),
     // then converge's (< t-min t) check (:201).
     {
-        BezWalk wk;
+        BezWalkT<TRACK> wk;
         bool busy = false;
         uint32_t si = 0, cursor = 0;
 #ifdef RT_STATS
@@ -841,8 +861,10 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                         const uint32_t e = W.sv[i];
                         si = i;
                         W.sz[i] = INFINITY;
-                        busy = TRACK ? bez_walk_begin_root(wk, ring[(rtail + i) & (uint32_t)(kBezRing - 1)], W.cl[e & 63u], W.lev[i])
-                                     : bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
+                        if constexpr (TRACK)
+                            busy = bez_walk_begin_root(wk, ring[(rtail + i) & (uint32_t)(kBezRing - 1)], W.cl[e & 63u], W.lev[i]);
+                        else
+                            busy = bez_walk_begin(wk, sc.bez[e >> 6], W.ray[e & 63u], W.cl[e & 63u], W.lev[i]);
                     }
                 }
                 cursor += (uint32_t)__popcll(idle);
@@ -863,7 +885,7 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
                     if (!busy && ir < nd) {
                         si = W.q[2 * ir];
                         const uint32_t e = W.sv[si], lr = W.q[2 * ir + 1];
-                        if (TRACK)
+                        if constexpr (TRACK)
                             bez_walk_take_root(wk, ring[(rtail + si) & (uint32_t)(kBezRing - 1)], W.cl[e & 63u], W.lev[si],
                                                lr >> 26, lr & ((1u << 26) - 1u));
                         else
@@ -1812,9 +1834,6 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // bvh_closest_curves; a ray finishes once its traversal has ended and every
 // curve candidate it queued has been resolved by a batch (W.done).
 // =====================================================================
-#ifndef RT_CURVE_WAVES
-#define RT_CURVE_WAVES 2               // waves per SIMD k_extend_curves is compiled for (VGPR budget 512 / waves)
-#endif
 static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK <= 160 * 1024 / RT_CURVE_WAVES,
               "k_extend_curves: RT_CURVE_WAVES blocks of BezWave state and LDS stack columns must fit a CU's LDS");
 #ifndef RT_CURVE_PREFETCH
