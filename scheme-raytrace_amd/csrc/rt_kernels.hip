@@ -716,10 +716,10 @@ constexpr int kBezQ = (RT_BEZ_QFLUSH > 64 ? RT_BEZ_QFLUSH : 64) + 64;   // < the
 #define RT_BEZ_HOLD 64                 // stage B runs once this many root-cull survivors wait (multiple of 64)
 #endif
 #ifndef RT_BEZ_LEAF_PHASE
-#define RT_BEZ_LEAF_PHASE 32           // stage B: lanes at a leaf segment that test together
+#define RT_BEZ_LEAF_PHASE 40           // stage B: lanes at a leaf segment that test together
 #endif
 #ifndef RT_CURVE_FINISH_BATCH
-#define RT_CURVE_FINISH_BATCH 16       // k_extend_curves: finished lanes written out and refilled together
+#define RT_CURVE_FINISH_BATCH 20       // k_extend_curves: finished lanes written out and refilled together
 #endif
 constexpr int kBezS = RT_BEZ_HOLD + kBezQ;   // survivors: < RT_BEZ_HOLD carried over + one stage A's worth
 static_assert(kBezS <= kBezRing && (kBezRing & (kBezRing - 1)) == 0,
