@@ -1854,7 +1854,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
     int gb = 0;                                     // the world BVH group (commit_scene builds at most one)
     while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
     bool active = false, exhausted = false, trav = false;
-    uint32_t k = 0, i = 0, queued = 0;
+    uint32_t i = 0, queued = 0;
     // The ray itself (o, d, time) is not kept in registers across iterations: the BVH step needs only
     // its box-test form and t scale, the sphere leaves and the finish reload it (ray_of below), so stage
     // B's walk state fits beside the loop's (registers cap the waves per SIMD, RT_CURVE_WAVES)
@@ -1956,12 +1956,15 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
             }
             active = false;
         }
-        const uint32_t slot = wave_append(cls, (k >> 8) & (uint32_t)(kShards - 1), counts, shard_cap);
+        // one shard per wave: the finishing lanes' appends take one returning atomic per class (a per-ray
+        // shard, k / 256, spread a batch over several shards, one dependent atomic each: -0.8 % at C5)
+        const uint32_t slot = wave_append(cls, (blockIdx.x * 4u + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1),
+                                          counts, shard_cap);
         if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
 #endif
-        // 2. free lanes take the next rays (virtual index k: shard = k / 256 as in k_extend)
+        // 2. free lanes take the next rays (claimed positions in the input queue)
         const unsigned long long need = __ballot(!active && !dead);
         if (need && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
@@ -1973,7 +1976,6 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
             if (!active && !dead) {
                 const uint32_t kk = base + lanes_below(need);
                 if (kk < n) {
-                    k = kk;
                     i = qphys(qm, kk);
                     v3 o, d;
                     double tm;
