@@ -94,7 +94,7 @@ def shade_roofline(ms_shade, launches, hits_d0, hits, survivors, note, scene):
     b = shade_bytes(hits_d0, hits, survivors)
     ach = b / (ms_shade * 1e-3) / 1e9
     hpl = (hits_d0 + hits) / launches
-    pm = load_pmc("pmc_shade.json", scene)      # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
+    pm, _ = load_pmc("shade", scene)            # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
     traffic = round(pm["bytes_per_hit"] * hpl) if pm and pm.get("bytes_per_hit") else None
     return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -130,6 +130,11 @@ def parse():
     p.add_argument("--no-profile-events", action="store_true")
     p.add_argument("--no-isolated", action="store_true", help="skip the single-lane profiling frame")
     p.add_argument("--lanes", type=int, default=0, help="render lanes (RT_OPT_LANES); 0 = the library's choice")
+    p.add_argument("--exact-libm", default="auto", choices=["auto", "exact", "device"],
+                   help="RT_OPT_EXACT_LIBM for the timed frames (bounce directions' sin / cos)")
+    p.add_argument("--shard-balance", default="",
+                   help="comma-separated shard counts (e.g. 2,4,8): render each tile shard of the frame alone on "
+                        "this GPU, print its time and segments (max / mean) and exit; no timed bench line")
     return p.parse_args()
 
 
@@ -261,7 +266,31 @@ def frame_rows_parity(o, frame_np, nx, ny, spp, seed, per_row_pass, budget_s, T)
             "pixels_gt_1e-9": int((d.reshape(-1, 3).max(axis=1) > 1e-9).sum()), "pixels": int(d.size // 3),
             "tolerance_rms": 1e-4, "pass": bool(rms <= 1e-4), "rows": "%d..%d" % (y0, y0 + rows - 1),
             "passes": "0..%d" % (spp - 1), "oracle_s": round(dt, 1),
-            "note": "rows of the last timed frame (the gathered frame on rank 0) vs the oracle, all passes"}
+            "note": "rows of the last timed frame (the gathered frame on rank 0) vs the oracle, all passes",
+            "_ref": ref[3 * lo:3 * hi]}
+
+
+def frame_rows_parity_mode(pf, scene, nx, ny, spp, seed, h, ctx, mode):
+    """parity_frame's rows again with RT_OPT_EXACT_LIBM = mode (rt_render_rows_device, every pass, the
+    production schedule), against the same oracle render (pf["_ref"])."""
+    import numpy as np
+    import torch
+    from rtamd import gpu
+    y0, y1 = (int(x) for x in pf["rows"].split(".."))
+    ref = pf.pop("_ref")
+    acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    with ctx.options(exact_libm=gpu._lib.RT_LIBM[mode]):
+        gpu.render_rows_device(scene, nx, ny, y0, y1 - y0 + 1, 0, spp, seed, acc.data_ptr(), ctx=ctx)
+    torch.cuda.synchronize()
+    lo, hi = 3 * y0 * nx, 3 * (y1 + 1) * nx
+    d = np.abs(acc.cpu().numpy()[lo:hi] / spp - ref / spp)
+    rms = float(np.sqrt(np.mean(d ** 2)))
+    return {"exact_libm": mode, "rms_vs_oracle": rms, "max_abs": float(d.max()),
+            "pixels_gt_1e-9": int((d.reshape(-1, 3).max(axis=1) > 1e-9).sum()), "pixels": int(d.size // 3),
+            "tolerance_rms": 1e-4, "pass": bool(rms <= 1e-4), "rows": pf["rows"], "passes": pf["passes"],
+            "note": "parity_frame's rows rendered again (rt_render_rows_device, production schedule) with "
+                    "RT_OPT_EXACT_LIBM = %s, against the same oracle render" % mode}
 
 
 def gpu_band_parity(scene, nx, ny, seed, ref, h, ctx):
@@ -295,6 +324,52 @@ def gpu_band_parity(scene, nx, ny, seed, ref, h, ctx):
             "note": "oracle = oracle/rt_oracle.c on the host, GPU = rt_render_rows_device (production schedule)"}
 
 
+def shard_balance(a, scene, h, ctx, nx, ny, spp, counts):
+    """--shard-balance: the multi-GPU frame's tile shards (rt_render_shard_device, tile t -> shard t % N)
+    rendered one at a time on this GPU, each timed alone, against the whole frame rendered the same way.
+    max / mean of the shard times bounds N-GPU strong-scaling efficiency (the frame waits for its slowest
+    rank); T_frame / max(T_shard) is the speedup the partition allows before the gather."""
+    import torch
+    from rtamd import dist as rdist
+    from rtamd import gpu
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t, gpu.stats(h)
+
+    frame = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    for _ in range(max(1, a.warmup)):
+        timed(lambda: gpu.render_device(scene, nx, ny, 0, spp, a.seed, frame.data_ptr(), stream=stream, ctx=ctx))
+    t_frame, st = timed(lambda: gpu.render_device(scene, nx, ny, 0, spp, a.seed, frame.data_ptr(), stream=stream,
+                                                  ctx=ctx))
+    out = {"mode": "shard_balance", "config": "%s: %s %dx%dx%dspp" % (SCENE_CONFIG.get(a.scene, "extra"), a.scene, nx,
+                                                                      ny, spp),
+           "frame_ms": round(t_frame * 1e3, 2), "frame_segments": int(st.segments), "partitions": {}}
+    for n in counts:
+        rows = []
+        for r in range(n):
+            shard = torch.zeros(rdist.local_size(nx, ny, r, n), dtype=torch.float64, device="cuda")
+            t, st = timed(lambda: gpu.render_shard_device(scene, nx, ny, 0, spp, a.seed, r, n, shard.data_ptr(),
+                                                          stream=stream, ctx=ctx))
+            rows.append({"shard": r, "pixels": shard.numel() // 3, "ms": round(t * 1e3, 2),
+                         "segments": int(st.segments)})
+            print("bench: shard-balance N=%d shard %d: %.1f ms" % (n, r, t * 1e3), file=sys.stderr, flush=True)
+        ms = [x["ms"] for x in rows]
+        sg = [x["segments"] for x in rows]
+        mean_ms, mean_sg = sum(ms) / n, sum(sg) / n
+        out["partitions"][str(n)] = {
+            "shards": rows, "ms_max_over_mean": round(max(ms) / mean_ms, 4),
+            "segments_max_over_mean": round(max(sg) / mean_sg, 4),
+            "predicted_speedup": round(t_frame * 1e3 / max(ms), 3),
+            "predicted_efficiency": round(t_frame * 1e3 / max(ms) / n, 4),
+            "note": "one GPU renders each shard alone: efficiency = T_frame / (N max T_shard), before the gather"}
+    print(json.dumps(out), flush=True)
+
+
 SCENE_CONFIG = {"cover": "C2", "cover_marble": "C3", "cornell": "C4", "cornell_mixture": "C4-mixture", "curves": "C5"}
 SCENE_DATA = {
     "cover": "RTIOW cover scene (random-scene, main.scm:31-89 + repairs R1/R3) generated from host seed 0x5EED0001",
@@ -314,16 +389,23 @@ def kernel_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def load_pmc(name, scene):
-    """profiles/<name> if it was measured on this scene with these kernels, else None."""
-    path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        pm = json.load(f)
-    if pm.get("scene") != scene or pm.get("kernel_sha16") != kernel_sha16():
-        return None
-    return pm
+def pmc_path(kind, scene):
+    """Where tools/pmc_report.py files a scene's PMC summary (kind: extend / shade)."""
+    return os.path.join(ROOT, "profiles", "pmc", "%s_%s.json" % (scene, kind))
+
+
+def load_pmc(kind, scene):
+    """The scene's PMC summary (profiles/pmc/<scene>_<kind>.json; profiles/pmc_<kind>.json, the C2 summary
+    of earlier rounds, as a fallback) if it was measured on this scene with these kernels, else None.
+    Returns (summary, path relative to the repo)."""
+    for path in (pmc_path(kind, scene), os.path.join(ROOT, "profiles", "pmc_%s.json" % kind)):
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            pm = json.load(f)
+        if pm.get("scene") == scene and pm.get("kernel_sha16") == kernel_sha16():
+            return pm, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def extend_roofline(segs, tail_segs, paths, launches, ms_ext, pm, kernels, note):
@@ -383,12 +465,31 @@ def main():
         else:
             dist.init_process_group(backend)
     nx, ny, spp = a.nx, a.ny, a.spp
-    scene = scenes.SCENES[a.scene](nx, ny)
+    t_scene = time.perf_counter()
+    scene = scenes.SCENES[a.scene](nx, ny)          # the host's scene constructors (the Scheme side's work)
+    t_scene = time.perf_counter() - t_scene
     ctx = gpu.default_context(device)
     if a.lanes:
         ctx.set_option("lanes", a.lanes)
-    h = gpu.upload(scene, ctx)                      # one-time scene upload (not timed)
+    ctx.set_option("exact_libm", a.exact_libm)
+    t_commit = time.perf_counter()
+    h = gpu.upload(scene, ctx)                      # one-time scene commit (not in the timed steps; reported)
+    t_commit = time.perf_counter() - t_commit
+    info0 = gpu.scene_info(h)
+    scene_commit = {
+        "scene_build_ms": round(t_scene * 1e3, 1),
+        "commit_total_ms": round(t_commit * 1e3, 1),
+        "constructors_ms": round(t_commit * 1e3 - info0["commit_ms"], 1),
+        "commit_build_ms": round(info0["commit_ms"] - info0["commit_upload_ms"], 1),
+        "commit_upload_ms": round(info0["commit_upload_ms"], 1),
+        "note": "one-time per scene, outside the timed steps (SURVEY §8(d) d1): scene_build = the host's scene "
+                "constructors (rtamd.scenes, e.g. points->bezier for C5); constructors = their rt_add_* calls "
+                "through the C ABI; commit_build = rt_scene_commit's flattening and BVH builds (SAH sweep, "
+                "BVH4 collapse); commit_upload = its device allocations and copies"}
     call("rt_set_profiling", h, 0 if a.no_profile_events else 1)
+    if a.shard_balance:
+        shard_balance(a, scene, h, ctx, nx, ny, spp, [int(x) for x in a.shard_balance.split(",") if x])
+        return
     # world == 1: the frame accumulator; world > 1: this rank's compact shard (its tiles only), gathered
     # onto rank 0 over RCCL at frame end (rtamd.dist.gather_frame).  Rank 0 resolves the frame to bytes
     # (main.scm:481-491) inside the step.
@@ -480,7 +581,7 @@ def main():
     if rank == 0:
         value = segs_all / elapsed / 1e6
         ext_kernels = extend_kernels(a.scene, gpu.scene_info(h))
-        pm = load_pmc("pmc_extend.json", a.scene)   # PMC counters of these kernels (tools/profile_round.sh)
+        pm, pm_src = load_pmc("extend", a.scene)    # PMC counters of these kernels (tools/profile_round.sh)
         two_lane = None
         if iso is not None:
             roof = extend_roofline(iso.segments, iso.segments - iso.extend_rays, iso.paths,
@@ -505,8 +606,7 @@ def main():
                           "lds_bank_conflict_ratio": round(pm["lds_bank_conflict_ratio"], 4),
                           "wait_share": round(pm["wait_share"], 4),
                           "valu_instr_per_segment": round(pm["valu_instr_per_segment"], 2),
-                          "source": "profiles/pmc_extend.json (%s, kernels %s)" % (pm.get("config", ""),
-                                                                                   pm["kernel_sha16"])}
+                          "source": "%s (%s, kernels %s)" % (pm_src, pm.get("config", ""), pm["kernel_sha16"])}
         if pm and roof and pm.get("f64_flops_per_segment"):
             tf = pm["f64_flops_per_segment"] * roof["rays_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
             valu = {"bound": "valu_f64", "achieved": round(tf, 3), "peak": F64_VALU_PEAK_TFLOPS,
@@ -544,10 +644,12 @@ def main():
                                if iso is not None else
                                shade_roofline(ms_shade, launches, sh_d0, sh, sh_surv, "timed region, one render lane",
                                               a.scene)),
-            "pmc_source": ("profiles/pmc_extend.json (kernels %s)" % pm["kernel_sha16"]) if pm else
+            "pmc_source": ("%s (kernels %s)" % (pm_src, pm["kernel_sha16"])) if pm else
                           "none: no PMC summary for these kernels (traffic / valu / valu_issue need "
                           "tools/profile_round.sh on this kernel source)",
             "scene_device": scene_device(gpu.scene_info(h)),
+            "scene_commit": scene_commit,
+            "exact_libm": a.exact_libm,
             "render_lanes": lanes,
             "per_rank_ms_per_step": {"render_min": round(min(render_s) * 1e3, 3),
                                      "render_max": round(max(render_s) * 1e3, 3),
@@ -583,6 +685,12 @@ def main():
                 out[k] = par[k]
             out["parity_frame"] = frame_rows_parity(o, last_frame, nx, ny, spp, a.seed, per_row_pass,
                                                     a.cpu_baseline_seconds, T)
+            # the same rows with the other libm mode (RT_OPT_EXACT_LIBM): exact = the C library's sin / cos
+            other = "device" if a.exact_libm == "exact" or (a.exact_libm == "auto" and a.scene == "curves") \
+                else "exact"
+            out["parity_frame_" + other] = frame_rows_parity_mode(out["parity_frame"], scene, nx, ny, spp, a.seed,
+                                                                  h, ctx, other)
+            out["parity_frame"]["exact_libm"] = a.exact_libm
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

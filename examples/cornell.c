@@ -3,14 +3,21 @@
  * of the reference would drive librtamd: constructors in the reference's
  * order, trace-all passes, resolve to 8-bit and a P3 PPM (main.scm:439-450).
  *
- *   gcc -O2 -Iinclude examples/cornell.c -Lscheme-raytrace_amd/rtamd -lrtamd \
+ *   gcc -O2 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ examples/cornell.c \
+ *       -Lscheme-raytrace_amd/rtamd -l:librtamd.so -L/opt/rocm/lib -lamdhip64 \
  *       -Wl,-rpath,$PWD/scheme-raytrace_amd/rtamd -o cornell
  *   ./cornell 128 128 16 cornell.ppm          (needs a GPU)
+ *   ./cornell 128 128 16 cornell.ppm gather   (the multi-GPU frame's path at world size 1: the
+ *                                              rank's tiles into a compact device accumulator,
+ *                                              rt_render_shard_device, then the frame-end RCCL
+ *                                              gather into the device frame, rt_gather_shards)
  *   ./cornell --abi                           (prints the ABI version; no GPU)
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "rt.h"
 
@@ -86,7 +93,37 @@ int main(int argc, char** argv) {
 
     double* accum = calloc((size_t)nx * ny * 3, sizeof(double));
     uint8_t* img = malloc((size_t)nx * ny * 3);
-    CHECK(rt_render(sc, nx, ny, 0, spp, 0x5EED0002ull, accum));     /* spp trace-all passes */
+    if (argc > 5 && strcmp(argv[5], "gather") == 0) {
+        /* one process of a multi-GPU frame (here world size 1): its communicator, its tiles into a
+         * compact device accumulator, the frame-end gather into rank 0's device frame */
+        const int rank = 0, world = 1;
+        uint8_t id[RT_COMM_ID_BYTES];
+        int comm;
+        CHECK(rt_comm_unique_id(id));                /* rank 0; a multi-process host ships it to the others */
+        CHECK(rt_comm_create(ctx, id, rank, world, &comm));
+        int64_t npix = 0;
+        CHECK(rt_shard_pixels(nx, ny, rank, world, NULL, &npix));
+        double *d_shard = NULL, *d_frame = NULL;
+        if (hipMalloc((void**)&d_shard, (size_t)npix * 3 * sizeof(double)) != hipSuccess ||
+            hipMalloc((void**)&d_frame, (size_t)nx * ny * 3 * sizeof(double)) != hipSuccess) {
+            fprintf(stderr, "hipMalloc failed\n");
+            return 1;
+        }
+        hipMemset(d_shard, 0, (size_t)npix * 3 * sizeof(double));
+        hipMemset(d_frame, 0, (size_t)nx * ny * 3 * sizeof(double));
+        hipDeviceSynchronize();
+        CHECK(rt_render_shard_device(sc, nx, ny, 0, spp, 0x5EED0002ull, rank, world, d_shard, NULL));
+        CHECK(rt_gather_shards(comm, nx, ny, d_shard, d_frame, NULL));
+        if (hipMemcpy(accum, d_frame, (size_t)nx * ny * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+            fprintf(stderr, "hipMemcpy failed\n");
+            return 1;
+        }
+        hipFree(d_shard);
+        hipFree(d_frame);
+        CHECK(rt_comm_destroy(comm));
+    } else {
+        CHECK(rt_render(sc, nx, ny, 0, spp, 0x5EED0002ull, accum));     /* spp trace-all passes */
+    }
     CHECK(rt_resolve_u8(accum, nx, ny, spp, img));
 
     FILE* f = fopen(out, "w");

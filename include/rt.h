@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -76,8 +76,21 @@ int rt_context_release_pools(int ctx);
  *   RT_OPT_TAIL_DIV   paths (B = the chunk's camera samples) finishes in the
  *                     persistent tail kernel; auto = 32768 and 256
  *   RT_OPT_TAIL_OFF   nonzero: no tail kernel, every depth in the wavefront
- *                     kernels (tests and A/B runs) */
-enum { RT_OPT_LANES = 1, RT_OPT_MAX_PATHS = 2, RT_OPT_TAIL_PATHS = 3, RT_OPT_TAIL_DIV = 4, RT_OPT_TAIL_OFF = 5 };
+ *                     kernels (tests and A/B runs)
+ * One option selects arithmetic, not the schedule:
+ *   RT_OPT_EXACT_LIBM the sin / cos of the lambertian bounce directions
+ *                     (random-cosine-direction, util.scm:37-44, and the light
+ *                     mixture's sphere sampler): RT_LIBM_EXACT = the reference
+ *                     runtime's C library bit for bit (glibc's algorithm,
+ *                     restated on the device), RT_LIBM_DEVICE = the device
+ *                     library (within 1 ulp, ~4.5 % faster on the cover scene),
+ *                     RT_LIBM_AUTO (0) = exact in scenes with curves (where an
+ *                     ulp of a bounce direction changes which ribbon a grazing
+ *                     ray hits), the device library elsewhere.  The marble
+ *                     texture's sin is exact in every mode. */
+enum { RT_OPT_LANES = 1, RT_OPT_MAX_PATHS = 2, RT_OPT_TAIL_PATHS = 3, RT_OPT_TAIL_DIV = 4, RT_OPT_TAIL_OFF = 5,
+       RT_OPT_EXACT_LIBM = 6 };
+enum { RT_LIBM_AUTO = 0, RT_LIBM_EXACT = 1, RT_LIBM_DEVICE = 2 };
 int rt_context_set_option(int ctx, int option, int64_t value);
 int rt_context_get_option(int ctx, int option, int64_t* out_value);
 
@@ -105,7 +118,8 @@ int rt_add_moving_sphere(int scene, const double center0[3], const double center
 int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1, double k,
                 int mat, int* out_obj);                                                          /* g:make-{xy,xz,yz}-rect :376-431 */
 /* cubic Bezier curve a,b,c,d of the given width (b:make-bezier bezier.scm:61); hit t is the distance
- * along unit(dir) and the normal is -dir (bezier.scm:176-214) */
+ * along unit(dir) and the normal is -dir (bezier.scm:176-214).  width: finite and nonzero (negative
+ * widths behave as in the reference: converge's boxes shrink by |width|/2) */
 int rt_add_bezier(int scene, const double a[3], const double b[3], const double c[3], const double d[3],
                   double width, int mat, int* out_obj);
 /* n curves at once (bezier->objs points.scm:45-53 over points->bezier output): cps holds n*12 doubles
@@ -198,6 +212,33 @@ int rt_render_shard_device(int scene, int nx, int ny, int spp_begin, int spp_cou
  * out_pix = NULL to get the count only. */
 int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* out_pix, int64_t* out_count);
 
+/* ---- multi-GPU frame (one process per GPU) ----------------
+ * Each rank renders its tiles with rt_render_shard_device into a compact
+ * accumulator; at frame end rt_gather_shards moves every rank's accumulator to
+ * rank 0 over RCCL (xGMI between the GPUs of a node) and places the pixels into
+ * rank 0's y-up frame.  Replaces nothing in the reference, which renders on one
+ * thread (main.scm:471-491, 633-634): it is the frame's only exchange step.
+ *
+ * rt_comm_unique_id: rank 0 makes the communicator's id (ncclGetUniqueId); the
+ *   host program ships the RT_COMM_ID_BYTES bytes to the other ranks (e.g.
+ *   over its own process group or a file).
+ * rt_comm_create: every rank, with the same id, its rank and the world size;
+ *   collective (returns once all ranks have called it).  The communicator
+ *   runs on the context's device.
+ * rt_gather_shards: every rank, collective.  accum_compact = the rank's
+ *   compact accumulator (device, 3 doubles per pixel of
+ *   rt_shard_pixels(nx, ny, rank, world)); frame_device = rank 0's nx*ny*3
+ *   frame (device; NULL on other ranks), whose pixels of every shard are
+ *   overwritten.  Enqueued on `stream` (NULL: the context's stream), which the
+ *   call synchronises before it returns.  The frame equals a one-process
+ *   rt_render_device of the same passes bit for bit (disjoint pixels, nothing
+ *   is summed). */
+#define RT_COMM_ID_BYTES 128
+int rt_comm_unique_id(uint8_t out_id[RT_COMM_ID_BYTES]);
+int rt_comm_create(int ctx, const uint8_t unique_id[RT_COMM_ID_BYTES], int rank, int world, int* out_comm);
+int rt_comm_destroy(int comm);
+int rt_gather_shards(int comm, int nx, int ny, const double* accum_compact, double* frame_device, void* stream);
+
 /* Errors raised on the device.  Every loop of the kernels that waits on data
  * (rejection samplers, curve subdivision walks, persistent kernels' per-path
  * loops) has an iteration cap a valid random stream cannot reach, and queue
@@ -214,6 +255,13 @@ enum { RT_FAULT_REJECT = 1, RT_FAULT_CURVE = 2, RT_FAULT_PATH = 4, RT_FAULT_SHAR
  * oracle's orc_hit_world); scenes with constant media are refused, since the
  * medium's hit test draws from the path's random stream. */
 int rt_hit_rays(int scene, int n, const double* rays, double* out_t, int32_t* out_mat);
+
+/* converge's subdivision depth (bezier.scm:179-193) as the curve kernels compute it (bez_maxd): for n
+ * curves given in ray space (cps = n x 12 doubles, the control points after bezier-transform) and 8 eps
+ * each (eps = width / 20), out_depth[i] = ceiling((log z) / (log 4)) with z = sqrt(2) n (n-1) l0 / (8 eps),
+ * 0 where the log is -inf, saturated at 25 (one past the 24 levels the walk supports; deeper curves fault
+ * the render).  A test probe of the device's log against the C library's. */
+int rt_curve_depth_probe(int ctx, int n, const double* cps, const double* eps8, int32_t* out_depth);
 
 /* Statistics of the last render on this scene. */
 typedef struct rt_stats {
@@ -252,6 +300,8 @@ typedef struct rt_scene_info {
     uint32_t camera_lds_bytes, camera_lds_blocks;   /* k_camera: the same */
     int32_t  cus;             /* compute units of the context's device */
     int32_t  curve_stack;     /* curve trees: stack entries the BVH4 walk of k_extend_curves may hold (0: none) */
+    double   commit_ms;       /* rt_scene_commit's wall time: flattening, BVH builds (SAH, BVH4 collapse), upload */
+    double   commit_upload_ms; /* of it: device allocations and host-to-device copies */
 } rt_scene_info;
 int rt_get_scene_info(int scene, rt_scene_info* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */

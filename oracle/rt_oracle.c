@@ -969,6 +969,10 @@ static int bvh_slab(const orc_bnode* nd, const double o[3], const double d[3], c
         }
         double ta = (nd->lo[a] - o[a]) * inv[a], tb = (nd->hi[a] - o[a]) * inv[a];
         if (ta > tb) { double t = ta; ta = tb; tb = t; }
+        /* the padding covers the rounding for origins near the scene; a ray may start anywhere (a curve
+         * reports its hit off the ribbon for |dir| != 1, Q10): widen by the origin's own share */
+        const double e = 0x1p-40 * fabs(o[a] * inv[a]);
+        ta -= e; tb += e;
         if (ta > t0) t0 = ta;
         if (tb < t1) t1 = tb;
     }

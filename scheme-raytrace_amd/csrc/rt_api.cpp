@@ -2,6 +2,7 @@
 // of the reference's object tree into grouped leaves, device upload and the
 // wavefront driver loop (raygen → [extend → shade/compact]* → accumulate).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -37,6 +38,8 @@ hipError_t launch_camera(const DevScene&, const RenderParams&, const PathState&,
 hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathState&, const QView&, uint32_t,
                              const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
+hipError_t launch_scatter_pixels(const double*, const uint32_t*, uint32_t, double*, hipStream_t);
+hipError_t launch_curve_depth(const double*, const double*, uint32_t, int32_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
 hipError_t take_curve_stats(unsigned long long out[2]);
 hipError_t launch_hit_rays(const DevScene&, const double*, uint32_t, double*, int32_t*, hipStream_t);
@@ -136,6 +139,7 @@ struct Context {
     int64_t opt_tail_paths = 0;                // RT_OPT_TAIL_PATHS (0: 32768)
     int64_t opt_tail_div = 0;                  // RT_OPT_TAIL_DIV (0: 256)
     bool wavefront_only = false;               // RT_OPT_TAIL_OFF: no tail kernel (tests, A/B)
+    int64_t opt_exact_libm = RT_LIBM_AUTO;     // RT_OPT_EXACT_LIBM: the bounce directions' sin / cos
 };
 
 struct Scene {
@@ -169,12 +173,26 @@ struct Scene {
     uint32_t pix_n = 0;
     bool profiling = false;
     rt_stats stats{};
+    double commit_ms = 0.0, commit_upload_ms = 0.0;   // rt_scene_commit: wall time, of it device allocation + copies
+};
+
+// A multi-GPU frame's communicator (rt_comm_create): one RCCL rank per process, bound to a context's
+// device.  Rank 0 keeps every rank's pixel list (rt_shard_pixels order, ranks concatenated) and a receive
+// buffer for the other ranks' compact accumulators, both kept for the frame size last gathered.
+struct Comm {
+    int ctx = -1, rank = 0, world = 1;
+    ncclComm_t nc = nullptr;
+    int nx = -1, ny = -1;
+    std::vector<int64_t> count, off;               // per rank: shard pixels and their offset in the lists
+    DevBuf pix, recv;
+    ~Comm() { if (nc) (void)ncclCommDestroy(nc); }
 };
 
 std::mutex g_mu;
 std::map<int, std::unique_ptr<Context>> g_ctx;
 std::map<int, std::unique_ptr<Scene>> g_scene;
-int g_next_ctx = 1, g_next_scene = 1;
+std::map<int, std::unique_ptr<Comm>> g_comm;
+int g_next_ctx = 1, g_next_scene = 1, g_next_comm = 1;
 
 Context* get_ctx(int h) {
     auto it = g_ctx.find(h);
@@ -452,12 +470,17 @@ size_t bvh_min_prims() {
     return e ? (size_t)std::strtoull(e, nullptr, 10) : 16;
 }
 
+// device time commit_scene spends in upload() (allocation + copy), for rt_scene_info's split of the
+// commit into host build and device upload
+thread_local double tl_upload_ms = 0.0;
 template <class T>
 int upload(DevBuf& b, const std::vector<T>& v, const T** out) {
+    const auto t0 = std::chrono::steady_clock::now();
     size_t n = std::max<size_t>(1, v.size()) * sizeof(T);
     HIPCHK(b.ensure(n));
     if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     *out = b.as<const T>();
+    tl_upload_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }
 
@@ -1266,8 +1289,15 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // for a third of it).  A floor of four cost 6.5 % on a 1/8-frame shard
     // (680x381x1024 spp, the per-rank work at 8 GPUs) and 2.4 % at 1/4
     // (profiles/r02/mc/).
-    // the cap is sized on the context's first render (before its pools exist), then kept
-    if (!c->pool_cap) c->pool_cap = max_paths(*c, std::min(kLanes, lanes_wanted(*c)));
+    // the cap is sized on the context's first render (before its pools exist), then kept; an option change
+    // that resets it (RT_OPT_LANES, RT_OPT_MAX_PATHS) frees the old pools first, so the sizing sees the
+    // memory they held and the lanes together stay within it
+    if (!c->pool_cap) {
+        for (auto& L : c->lanes)
+            if (L && L->stream) HIPCHK(hipStreamSynchronize(L->stream));
+        for (auto& L : c->lanes) L.reset();
+        c->pool_cap = max_paths(*c, std::min(kLanes, lanes_wanted(*c)));
+    }
     const size_t cap_paths = c->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
     if (chunk > (uint32_t)spp_count) chunk = (uint32_t)spp_count;
@@ -1287,7 +1317,11 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // blocks of one shard can append in one wavefront step (extend: one item
     // per thread; the four shade kernels: grid-stride over at most 4096 blocks)
     const size_t gmax = std::min<size_t>(4096, (cap + 255) / 256 + kShards);
-    const size_t shard_cap = (cap + kShards - 1) / kShards + 4 * 32 * gmax + 256;
+    size_t slack = 4 * 32 * gmax + 256;
+    // test switch (RTAMD_SHARD_SLACK): a smaller slack drives k_extend_curves' hit appends past their wave's
+    // shard (wave_append<true> spills into the next one); 256 still bounds the shade kernels' survivors
+    if (const char* e = std::getenv("RTAMD_SHARD_SLACK")) slack = std::max<size_t>(256, std::strtoull(e, nullptr, 10));
+    const size_t shard_cap = (cap + kShards - 1) / kShards + slack;
     const size_t scap = shard_cap * kShards;
     if (scap >= (1ull << 32)) return fail("path pool too large");
     constexpr int kCountsPerIter = 5 * kShards * kCntStride;   // 4 material hit queues + survivors, 8 shards each
@@ -1332,6 +1366,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         }
     } drain{c, nlanes};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    // RT_OPT_EXACT_LIBM: auto = exact in scenes with curves ("libm")
+    const bool exact_libm = c->opt_exact_libm == RT_LIBM_EXACT || (c->opt_exact_libm == RT_LIBM_AUTO && s->dev.n_bez > 0);
     uint64_t seq = 0;
 
     // Enqueue the lane's next step for its current path count: one wavefront
@@ -1415,7 +1451,9 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             n += c_x;
         }
         uint64_t hits = 0;
-        for (int k = 0; k < 4 * kShards; ++k) hits += row[k * kCntStride];
+        // a hit-queue counter can pass its shard's capacity (k_extend_curves' items then spill into the next
+        // shard): what the queue holds is the clamped count
+        for (int k = 0; k < 4 * kShards; ++k) hits += std::min<uint32_t>(row[k * kCntStride], (uint32_t)shard_cap);
         (L.depth == 0 ? s->stats.shade_hits_d0 : s->stats.shade_hits) += hits;
         s->stats.shade_survivors += n;
         L.view = QView{L.counts.as<uint32_t>() + L.depth * kCountsPerIter + 4 * kShards * kCntStride,
@@ -1438,6 +1476,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         rp.sb = L.sb.as<double>();
         rp.B = npix * L.S;
         rp.compact = compact ? 1u : 0u;
+        rp.exact_libm = exact_libm ? 1u : 0u;
         HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
         const uint32_t tail = tail_paths(*c, rp.B);
         L.fused_camera = s->cam_lds != 0 && rp.B > tail;     // the tail kernel starts from raygen's state
@@ -1586,6 +1625,7 @@ int rt_context_set_option(int ctx, int option, int64_t value) {
     switch (option) {
     case RT_OPT_LANES:
         if (value > kLanes) return fail("RT_OPT_LANES: at most " + std::to_string(kLanes) + " render lanes");
+        if (value != c->opt_lanes) c->pool_cap = 0;   // the pools are sized for the lanes together: again
         c->opt_lanes = value;
         break;
     case RT_OPT_MAX_PATHS:
@@ -1596,6 +1636,10 @@ int rt_context_set_option(int ctx, int option, int64_t value) {
     case RT_OPT_TAIL_PATHS: c->opt_tail_paths = value; break;
     case RT_OPT_TAIL_DIV: c->opt_tail_div = value; break;
     case RT_OPT_TAIL_OFF: c->wavefront_only = value != 0; break;
+    case RT_OPT_EXACT_LIBM:
+        if (value > RT_LIBM_DEVICE) return fail("RT_OPT_EXACT_LIBM: RT_LIBM_AUTO, RT_LIBM_EXACT or RT_LIBM_DEVICE");
+        c->opt_exact_libm = value;
+        break;
     default: return fail("unknown context option " + std::to_string(option));
     }
     return 0;
@@ -1612,6 +1656,7 @@ int rt_context_get_option(int ctx, int option, int64_t* out) {
     case RT_OPT_TAIL_PATHS: *out = c->opt_tail_paths; break;
     case RT_OPT_TAIL_DIV: *out = c->opt_tail_div; break;
     case RT_OPT_TAIL_OFF: *out = c->wavefront_only ? 1 : 0; break;
+    case RT_OPT_EXACT_LIBM: *out = c->opt_exact_libm; break;
     default: return fail("unknown context option " + std::to_string(option));
     }
     return 0;
@@ -1721,7 +1766,9 @@ int rt_add_bezier(int scene, const double a[3], const double b[3], const double 
     OUT_OR_FAIL(out);
     if (!a || !b || !c || !d) return fail("rt_add_bezier: null control point");
     if (check_mat(s, mat)) return 1;
-    if (!(width > 0.0) || !std::isfinite(width)) return fail("rt_add_bezier: width must be positive and finite");
+    // any finite nonzero width, negative ones too (make-bezier has no check; width1 = width / 2 then
+    // shrinks converge's boxes and a hit needs |p.xy| < |width1|); zero would divide in the depth estimate
+    if (width == 0.0 || !std::isfinite(width)) return fail("rt_add_bezier: width must be finite and nonzero");
     Obj o; o.type = O_BEZIER; o.mat = mat; o.width = width;
     const double* p[4] = {a, b, c, d};
     for (int i = 0; i < 4; ++i) for (int k = 0; k < 3; ++k) o.cp[3 * i + k] = p[i][k];
@@ -1732,7 +1779,9 @@ int rt_add_bezier_array(int scene, const double* cps, int n, double width, int m
     OUT_OR_FAIL(out_first);
     if (n < 0 || (n > 0 && !cps)) return fail("rt_add_bezier_array: invalid curve array");
     if (check_mat(s, mat)) return 1;
-    if (!(width > 0.0) || !std::isfinite(width)) return fail("rt_add_bezier_array: width must be positive and finite");
+    // any finite nonzero width, negative ones too (make-bezier has no check; width1 = width / 2 then
+    // shrinks converge's boxes and a hit needs |p.xy| < |width1|); zero would divide in the depth estimate
+    if (width == 0.0 || !std::isfinite(width)) return fail("rt_add_bezier_array: width must be finite and nonzero");
     *out_first = (int)s->objs.size();
     s->objs.reserve(s->objs.size() + (size_t)n);
     for (int i = 0; i < n; ++i) {
@@ -1897,7 +1946,12 @@ int rt_set_perlin_tables(int scene, const double ranvec[768], const int32_t px[2
 int rt_scene_commit(int scene, int world) {
     SCENE_OR_FAIL(s, scene);
     if (check_obj(s, world)) return 1;
-    return commit_scene(s, world);
+    const auto t0 = std::chrono::steady_clock::now();
+    tl_upload_ms = 0.0;
+    const int rc = commit_scene(s, world);
+    s->commit_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    s->commit_upload_ms = tl_upload_ms;
+    return rc;
 }
 
 int rt_set_profiling(int scene, int enabled) {
@@ -1941,6 +1995,8 @@ int rt_get_scene_info(int scene, rt_scene_info* out) {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
     out->cus = cus;
     out->curve_stack = d.bvh4 ? d.stack4 : 0;
+    out->commit_ms = s->commit_ms;
+    out->commit_upload_ms = s->commit_upload_ms;
     return 0;
 }
 
@@ -1971,6 +2027,27 @@ int rt_hit_rays(int scene, int n, const double* rays, double* out_t, int32_t* ou
     uint32_t f = 0;
     HIPCHK(take_fault(&f));
     if (f) return fail(fault_text(f));
+    return 0;
+}
+
+int rt_curve_depth_probe(int ctx, int n, const double* cps, const double* eps8, int32_t* out_depth) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    if (n < 0) return fail("curve count must be >= 0");
+    if (n == 0) return 0;
+    if (!cps || !eps8 || !out_depth) return fail("null pointer");
+    HIPCHK(hipSetDevice(c->device));
+    DevBuf d_cps, d_eps, d_out;
+    HIPCHK(d_cps.ensure((size_t)n * 12 * sizeof(double)));
+    HIPCHK(d_eps.ensure((size_t)n * sizeof(double)));
+    HIPCHK(d_out.ensure((size_t)n * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(d_cps.p, cps, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_eps.p, eps8, (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_curve_depth(d_cps.as<const double>(), d_eps.as<const double>(), (uint32_t)n, d_out.as<int32_t>(),
+                              c->stream));
+    HIPCHK(hipMemcpyAsync(out_depth, d_out.p, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 
@@ -2094,6 +2171,118 @@ int rt_resolve_u8(const double* accum, int nx, int ny, int count, uint8_t* out) 
         const double m = (1.0 < c) ? 1.0 : c;
         out[i] = (uint8_t)std::floor(255.99 * m);
     }
+    return 0;
+}
+
+// ---- multi-GPU frame: the frame-end gather over RCCL (include/rt.h) ----
+#define NCCLCHK(expr)                                                                  \
+    do {                                                                               \
+        ncclResult_t r_ = (expr);                                                      \
+        if (r_ != ncclSuccess) return fail(std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int rt_comm_unique_id(uint8_t out_id[RT_COMM_ID_BYTES]) {
+    if (!out_id) return fail("null out pointer");
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RT_COMM_ID_BYTES is RCCL's unique id size");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(out_id, &id, sizeof id);
+    return 0;
+}
+
+int rt_comm_create(int ctx, const uint8_t unique_id[RT_COMM_ID_BYTES], int rank, int world, int* out_comm) {
+    if (!unique_id || !out_comm) return fail("null pointer");
+    if (world <= 0 || rank < 0 || rank >= world) return fail("invalid rank / world size");
+    int device = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context* c = get_ctx(ctx);
+        if (!c) return fail("invalid context handle");
+        device = c->device;
+    }
+    HIPCHK(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof id);
+    auto m = std::make_unique<Comm>();
+    m->ctx = ctx; m->rank = rank; m->world = world;
+    // collective: returns once every rank has called it (outside the lock: it waits for the other processes)
+    NCCLCHK(ncclCommInitRank(&m->nc, world, id, rank));
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int h = g_next_comm++;
+    g_comm[h] = std::move(m);
+    *out_comm = h;
+    return 0;
+}
+
+int rt_comm_destroy(int comm) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_comm.find(comm);
+    if (it == g_comm.end()) return fail("invalid communicator handle");
+    Context* c = get_ctx(it->second->ctx);
+    if (c) HIPCHK(hipSetDevice(c->device));
+    g_comm.erase(it);
+    return 0;
+}
+
+int rt_gather_shards(int comm, int nx, int ny, const double* accum_compact, double* frame_device, void* stream) {
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
+    Comm* m = nullptr;
+    Context* c = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_comm.find(comm);
+        if (it == g_comm.end()) return fail("invalid communicator handle");
+        m = it->second.get();
+        c = get_ctx(m->ctx);
+        if (!c) return fail("the communicator's context was destroyed");
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (m->nx != nx || m->ny != ny) {                  // the shards' pixel lists for this frame size
+        m->nx = -1;
+        m->count.assign(m->world, 0);
+        m->off.assign(m->world, 0);
+        std::vector<uint32_t> all;
+        for (int r = 0; r < m->world; ++r) {
+            const std::vector<uint32_t> pl = make_pixlist(nx, ny, PixSel{0, ny, r, m->world});
+            m->off[r] = (int64_t)all.size();
+            m->count[r] = (int64_t)pl.size();
+            if (m->rank == 0) all.insert(all.end(), pl.begin(), pl.end());
+        }
+        if (m->rank == 0) {
+            HIPCHK(m->pix.ensure(std::max<size_t>(1, all.size()) * sizeof(uint32_t)));
+            HIPCHK(hipMemcpy(m->pix.p, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            const size_t others = all.size() - (size_t)m->count[0];
+            HIPCHK(m->recv.ensure(std::max<size_t>(1, others) * 3 * sizeof(double)));
+        }
+        m->nx = nx; m->ny = ny;
+    }
+    const int64_t mine = m->count[m->rank];
+    if (mine > 0 && !accum_compact) return fail("null compact accumulator");
+    if (m->rank == 0 && !frame_device) return fail("rank 0 needs the frame buffer");
+    // RCCL has no gather: every other rank sends its compact accumulator (its exact size, no padding) to
+    // rank 0, which posts one receive per rank into its buffer, in one group
+    if (m->world > 1) {
+        NCCLCHK(ncclGroupStart());
+        if (m->rank != 0) {
+            if (mine > 0) NCCLCHK(ncclSend(accum_compact, (size_t)(3 * mine), ncclDouble, 0, m->nc, st));
+        } else {
+            double* recv = m->recv.as<double>();
+            for (int r = 1; r < m->world; ++r)
+                if (m->count[r] > 0)
+                    NCCLCHK(ncclRecv(recv + 3 * (m->off[r] - m->count[0]), (size_t)(3 * m->count[r]), ncclDouble, r,
+                                     m->nc, st));
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
+    if (m->rank == 0) {                                // place every shard's pixels into the y-up frame
+        const uint32_t* pix = m->pix.as<const uint32_t>();
+        HIPCHK(launch_scatter_pixels(accum_compact, pix, (uint32_t)m->count[0], frame_device, st));
+        const int64_t others = m->off[m->world - 1] + m->count[m->world - 1] - m->count[0];
+        HIPCHK(launch_scatter_pixels(m->recv.as<const double>(), pix + m->count[0], (uint32_t)others, frame_device, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
 

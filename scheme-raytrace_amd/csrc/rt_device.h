@@ -257,6 +257,8 @@ struct RenderParams {
     double* sb;               // sample colours [B][3] (one rgb record per work id), B = npix * chunk_spp
     uint32_t B;
     uint32_t compact;         // accumulator indexed by shard pixel q (rt_render_shard_device), not image pixel j
+    uint32_t exact_libm;      // host side: lambertian bounce directions with rt_libm.h's sin / cos (RT_OPT_EXACT_LIBM;
+                              // launch_shade / launch_finish pick the kernel instance by it)
     double inx, iny;          // RN(1/nx), RN(1/ny): trace-all's (/ (+ i r) nx) as div_ia (rt_kernels.hip)
 };
 

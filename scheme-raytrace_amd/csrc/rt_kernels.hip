@@ -31,6 +31,7 @@
 #include "rt_device.h"
 #include "rt_libm.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace rtamd {
 
@@ -110,27 +111,28 @@ __device__ __forceinline__ double div_ia(const double x, const double a, const d
 
 // ------------------------------------------------------------ vec.scm
 // sin / cos as the reference's libm computes them (rt_libm.h); OCML beyond the
-// reference algorithm's reduction range, which no argument on the path reaches
-__device__ __forceinline__ double rt_sin(const double x) { return rtlibm::sin_(x); }
-__device__ __forceinline__ double rt_cos(const double x) { return rtlibm::cos_(x); }
+// reference algorithm's reduction range (|x| >= 0x1.921fbp+26 = 105414336, inf, nan)
+__device__ __forceinline__ double rt_sin(const double x) { return rtlibm::sin_full(x); }
+__device__ __forceinline__ double rt_cos(const double x) { return rtlibm::cos_full(x); }
 // cos(a) and sin(b), one evaluation after the other: inlined side by side, the two would hold their
 // temporaries at once (the shade kernels' register budget)
 __device__ __forceinline__ void rt_cos_sin(const double a, const double b, double& c, double& s, const double* tab) {
     double v0 = 0.0, v1 = 0.0;
 #pragma unroll 1
     for (int j = 0; j < 2; ++j) {
-        const double v = rtlibm::sincos_(j == 0 ? a : b, j == 0, tab);
+        const double v = rtlibm::sincos_full(j == 0 ? a : b, j == 0, tab);
         if (j == 0) v0 = v; else v1 = v;
     }
     c = v0;
     s = v1;
 }
 // The bounce directions' cos / sin (random-cosine-direction, util.scm:37-44; the light mixture's
-// random-to-sphere): EX = libm's own bits (rt_libm.h), else OCML's (within 1 ulp).  Scenes with curves
+// random-to-sphere): EX = libm's own bits (rt_libm.h), else OCML's (within 1 ulp).  The render's
+// RT_OPT_EXACT_LIBM picks the kernel instance (RenderParams::exact_libm); by default scenes with curves
 // take EX: a grazing ribbon hit turns a 1-ulp direction change into another path (the dense flat-curve
-// test); elsewhere OCML's ulps move pixels by ~1e-16 (C2 band RMS 1.6e-13) and EX would cost C2 ~4.5 %
-// (profiles/r04/ab_libm_c2.log).  Marble textures use rt_libm.h in every scene (checker_odd needs
-// only a sine's sign).
+// test); elsewhere OCML's ulps move pixels by ~1e-16 (C2 band RMS 1.6e-13, a few horizon pixels by up
+// to 1e-6) and EX costs C2 ~4.5 % (profiles/r04/ab_libm_c2.log).  Marble textures use rt_libm.h in
+// every scene (checker_odd needs only a sine's sign).
 template <bool EX>
 __device__ __forceinline__ void bounce_cos_sin(const double a, const double b, double& c, double& s, const double* tab) {
     if (EX) {
@@ -386,7 +388,8 @@ __device__ __forceinline__ bool bez_sep_axis(const Bez4& c, const v3 a, const v3
 __device__ __forceinline__ double bez_hull_r2(const Bez4& c, const double w1) {
     const double s = fmax(fmax(fmax(fabs(c.p0.x), fabs(c.p0.y)), fmax(fabs(c.p1.x), fabs(c.p1.y))),
                           fmax(fmax(fabs(c.p2.x), fabs(c.p2.y)), fmax(fabs(c.p3.x), fabs(c.p3.y))));
-    const double r = fma(w1, 1e-9, w1) + 1e-9 * s;
+    const double aw = fabs(w1);         // a hit needs |p.xy|^2 < width2 = w1^2: |w1| for a negative width too
+    const double r = fma(aw, 1e-9, aw) + 1e-9 * s;
     return r * r;
 }
 template <int EDGES>
@@ -1020,6 +1023,32 @@ __device__ __forceinline__ BoxRay box_ray(const v3 o, const v3 d) {
     b.px = (float)(o.x * ix); b.py = (float)(o.y * iy); b.pz = (float)(o.z * iz);
     return b;
 }
+// Rays from anywhere (scenes with curves).  The box margin covers the slab ends' rounding only for an
+// origin inside the scene radius, but a curve reports its hit at the distance along unit(dir) on the raw
+// ray (Q10, bezier.scm:204-206), so a ray with |dir| != 1 (a reflection off a metal curve: |dir| grows
+// ~quadratically per bounce) starts its next segment far outside the scene: at 1e9 from it, a C5-style
+// scene's f32 slab ends err by more than the margin, and the walk culled a curve the ray hits
+// (test_few_curves_among_spheres_large_launch, pixel 247288 sample 5, segment 70).  The rounding that
+// depends on the origin is below 4 ulps of |o / d| per axis, so this box ray subtracts o/d - e from
+// the near plane of each axis and o/d + e from the far one, e = 2^-20 |o / d| (about 8x that bound):
+// each slab is widened by its own error, at no extra instruction in the node test (the lo and hi
+// planes take different registers instead of one).
+struct BoxRayW { float ix, iy, iz, lx, ly, lz, hx, hy, hz; };   // 1/d; o/d adjusted for the lo / hi planes
+__device__ __forceinline__ BoxRayW box_ray_w(const v3 o, const v3 d) {
+    const double lim = 1e30;
+    const double i[3] = {fmax(fmin(1.0 / d.x, lim), -lim), fmax(fmin(1.0 / d.y, lim), -lim),
+                         fmax(fmin(1.0 / d.z, lim), -lim)};
+    const double oo[3] = {o.x, o.y, o.z};
+    float lo[3], hi[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double p = oo[a] * i[a], e = 0x1p-20 * fabs(p);
+        // ix >= 0: the lo plane gives the near end (subtract more), the hi plane the far one; else swapped
+        lo[a] = (float)(i[a] >= 0.0 ? p + e : p - e);
+        hi[a] = (float)(i[a] >= 0.0 ? p - e : p + e);
+    }
+    return BoxRayW{(float)i[0], (float)i[1], (float)i[2], lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+}
 // Both child boxes of N (interleaved planes, BvhNode2): slab ends t = fma(box,
 // 1/d, -o/d), near / far per child; hit iff near <= far.  (Packed v_pk_fma_f32
 // pairs were measured slower here: the pairs raise register pressure.)
@@ -1029,6 +1058,20 @@ __device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRay& r, con
         const float tx0 = fmaf(N.b[0 + c], r.ix, -r.px), tx1 = fmaf(N.b[6 + c], r.ix, -r.px);
         const float ty0 = fmaf(N.b[2 + c], r.iy, -r.py), ty1 = fmaf(N.b[8 + c], r.iy, -r.py);
         const float tz0 = fmaf(N.b[4 + c], r.iz, -r.pz), tz1 = fmaf(N.b[10 + c], r.iz, -r.pz);
+        tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
+        return tn <= tf;
+    };
+    hl = one(0, tl);
+    hr = one(1, tr);
+}
+// the same with the widened slabs of a box ray from anywhere (BoxRayW)
+__device__ __forceinline__ void node_hit(const BvhNode2& N, const BoxRayW& r, const float tcap, bool& hl, bool& hr,
+                                         float& tl, float& tr) {
+    auto one = [&](const int c, float& tn) {
+        const float tx0 = fmaf(N.b[0 + c], r.ix, -r.lx), tx1 = fmaf(N.b[6 + c], r.ix, -r.hx);
+        const float ty0 = fmaf(N.b[2 + c], r.iy, -r.ly), ty1 = fmaf(N.b[8 + c], r.iy, -r.hy);
+        const float tz0 = fmaf(N.b[4 + c], r.iz, -r.lz), tz1 = fmaf(N.b[10 + c], r.iz, -r.hz);
         tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
         const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
         return tn <= tf;
@@ -1086,7 +1129,8 @@ __device__ __forceinline__ int32_t stack_ref(const uint16_t e) { return (int32_t
 // DIRECT (FROZEN only, DevScene::bvh_solo): every time-0 leaf holds one
 // sphere and fsph is in leaf order, so leaf ref ~k tests fsph[k] directly
 // (no leaf record to fetch or keep in LDS).
-template <bool FROZEN, class SE = uint32_t, bool DIRECT = false>
+// WIDE: the box ray from anywhere (BoxRayW; scenes with curves, whose rays may start far outside)
+template <bool FROZEN, class SE = uint32_t, bool DIRECT = false, bool WIDE = false>
 __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o, const v3 d, const double time,
                                                  double& closest, int32_t& best, SE* lstk, const int lmax,
                                                  const BvhNode2* __restrict__ nodes,
@@ -1097,10 +1141,15 @@ __device__ __forceinline__ void bvh_closest_lane(const DevScene& sc, const v3 o,
                                                  const int32_t* __restrict__ fid = nullptr) {
     constexpr int32_t kDone = INT32_MIN;
     const double a = dot(d, d), ia = 1.0 / a;
-    const BoxRay br = box_ray(o, d);
     // 16-bit stacks: the LDS-tree walks; RT_SIGNED_SLAB 1 = the time-0 tree only, 2 = also the all-times tree
     constexpr bool SIGNED = sizeof(SE) == 2 && (RT_SIGNED_SLAB == 2 || (RT_SIGNED_SLAB == 1 && FROZEN));
-    const SlabPtr slp = slab_ptr(nodes, slab_off(br));
+    static_assert(!(WIDE && SIGNED), "the sign-selected LDS walks serve scenes without curves only");
+    using BR = typename std::conditional<WIDE, BoxRayW, BoxRay>::type;
+    BR br;
+    if constexpr (WIDE) br = box_ray_w(o, d);
+    else br = box_ray(o, d);
+    SlabPtr slp{};
+    if constexpr (SIGNED) slp = slab_ptr(nodes, slab_off(br));
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
     const uint32_t stride = blockDim.x;
     int32_t fbest = -1;                                       // FROZEN: fsph index of the best hit
@@ -1230,7 +1279,7 @@ __device__ __forceinline__ void bvh_closest_curves(const DevScene& sc, const v3 
                                                 double& closest, int32_t& best, uint32_t* lstk, const int lmax,
                                                 BezWave& W) {
     const double a = dot(d, d), ia = 1.0 / a;
-    const BoxRay br = box_ray(o, d);
+    const BoxRayW br = box_ray_w(o, d);              // rays from anywhere (BoxRayW)
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     const double tscale = fmax(1.0, 1.0 / sqrt(a));
     const uint32_t lane = threadIdx.x & 63u;
@@ -1564,10 +1613,10 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& sc, const v3 o0, 
             if (BEZ && sc.bvh_has_bez)
                 bvh_closest_curves(sc, o0, d0, time, closest, best, reinterpret_cast<uint32_t*>(lstk), lmax, *bw);
             else if (sc.fbvh2 && (sc.tree0_any_time || __double_as_longlong(time) == 0ll))   // the time-0 tree
-                bvh_closest_lane<true, SE>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves, t0.sph,
-                                           nullptr, nullptr, t0.fid);
-            else bvh_closest_lane<false, SE>(sc, o0, d0, time, closest, best, lstk, lmax, ta.nodes, ta.leaves, nullptr,
-                                         ta.sph, ta.msph);
+                bvh_closest_lane<true, SE, false, BEZ>(sc, o0, d0, time, closest, best, lstk, lmax, t0.nodes, t0.leaves,
+                                                       t0.sph, nullptr, nullptr, t0.fid);
+            else bvh_closest_lane<false, SE, false, BEZ>(sc, o0, d0, time, closest, best, lstk, lmax, ta.nodes, ta.leaves,
+                                                     nullptr, ta.sph, ta.msph);
             continue;
         }
         group_closest<F>(sc, G, o0, d0, time, closest, best, rng);
@@ -1799,11 +1848,17 @@ __global__ __launch_bounds__(256) void k_hit_rays(const DevScene sc, const doubl
 // class c, shard x -> counter (c * kShards + x), slot x * shard_cap + rank)
 // for kernels whose lanes finish at different loop iterations.  One atomic
 // per distinct (class, shard) among the wave's finishing lanes.
+// SPILL: the shard is the caller's choice and not bounded by it (k_extend_curves picks one per wave, and
+// its waves claim rays dynamically), so an item that finds its shard full moves on to the next shard, up
+// to all kShards of them (together they hold every item of the launch).  The full shard's entries below
+// its capacity were all written (the lanes that got them), so the consumers' clamped counts stay exact.
+template <bool SPILL = false>
 __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t shard, uint32_t* __restrict__ counts,
                                                 const uint32_t shard_cap) {
     const uint32_t lane = threadIdx.x & 63u;
     bool pending = cls >= 0;
-    const uint32_t key = pending ? (uint32_t)cls * kShards + shard : 0u;
+    uint32_t key = pending ? (uint32_t)cls * kShards + shard : 0u;
+    uint32_t tries = 0;
     uint32_t slot = 0;
     unsigned long long m = __ballot(pending);
     while (m) {
@@ -1816,9 +1871,16 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
         base = (uint32_t)__shfl((int)base, leader, 64);
         if (mine) {
             const uint32_t local = base + lanes_below(mk);
-            if (local < shard_cap) slot = (K % kShards) * shard_cap + local;
-            else { raise_fault(RT_FAULT_SHARD); slot = kNoSlot; }  // never write past the shard
-            pending = false;
+            if (local < shard_cap) {
+                slot = (K % kShards) * shard_cap + local;
+                pending = false;
+            } else if (SPILL && ++tries < (uint32_t)kShards) {
+                key = (K / kShards) * kShards + ((K + 1u) % kShards);     // the same class, the next shard
+            } else {
+                raise_fault(RT_FAULT_SHARD);                              // never write past the shard
+                slot = kNoSlot;
+                pending = false;
+            }
         }
         m = __ballot(pending);
     }
@@ -1863,7 +1925,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
     // best's material class (leaf_cls), loaded whenever best changes: the load is in flight while the
     // traversal goes on, not a round trip of the finish
     int32_t bcls = -1;
-    BoxRay br{};
+    BoxRayW br{};                                   // rays from anywhere (BoxRayW)
 #if RT_CURVE_PREFETCH
     BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
 #endif
@@ -1957,9 +2019,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
             active = false;
         }
         // one shard per wave: the finishing lanes' appends take one returning atomic per class (a per-ray
-        // shard, k / 256, spread a batch over several shards, one dependent atomic each: -0.8 % at C5)
-        const uint32_t slot = wave_append(cls, (blockIdx.x * 4u + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1),
-                                          counts, shard_cap);
+        // shard, k / 256, spread a batch over several shards, one dependent atomic each: -0.8 % at C5).
+        // Waves claim rays dynamically, so a shard's share is not bounded by n / kShards: a full shard
+        // spills into the next (wave_append<true>)
+        const uint32_t slot = wave_append<true>(cls, (blockIdx.x * 4u + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1),
+                                                counts, shard_cap);
         if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
@@ -1984,7 +2048,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                     best = -1;
                     for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
                     bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
-                    br = box_ray(o, d);
+                    br = box_ray_w(o, d);
                     tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
                     bez_ray(o, d, W.ray[lane]);
                     W.done[lane] = 0u;
@@ -2014,9 +2078,9 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                 int32_t ref[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float tx0 = fmaf(N.lo[0][j], br.ix, -br.px), tx1 = fmaf(N.hi[0][j], br.ix, -br.px);
-                    const float ty0 = fmaf(N.lo[1][j], br.iy, -br.py), ty1 = fmaf(N.hi[1][j], br.iy, -br.py);
-                    const float tz0 = fmaf(N.lo[2][j], br.iz, -br.pz), tz1 = fmaf(N.hi[2][j], br.iz, -br.pz);
+                    const float tx0 = fmaf(N.lo[0][j], br.ix, -br.lx), tx1 = fmaf(N.hi[0][j], br.ix, -br.hx);
+                    const float ty0 = fmaf(N.lo[1][j], br.iy, -br.ly), ty1 = fmaf(N.hi[1][j], br.iy, -br.hy);
+                    const float tz0 = fmaf(N.lo[2][j], br.iz, -br.lz), tz1 = fmaf(N.hi[2][j], br.iz, -br.hz);
                     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
                     key[j] = (tn <= tf && j < N.n) ? tn : INFINITY;   // slab ends are finite: INFINITY = missed
@@ -2766,7 +2830,7 @@ __global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScen
 #endif                                // (the compiler's choice is 143: 3 waves; the other variants would spill at 128)
 template <int F, bool PN, bool LSM>
 constexpr int finish_waves() { return (F == 0 && !PN && !LSM) ? RT_FINISH_WAVES : 1; }
-template <int F, bool PN, bool LSM, bool SOLO = false>
+template <int F, bool PN, bool LSM, bool SOLO = false, bool EX = false>
 __global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(const DevScene* __restrict__ scp, const RenderParams rp, const PathState st,
                                                 const QView in, uint32_t n,
                                                 unsigned long long* __restrict__ tail_ctl, int tree0_lds,
@@ -2849,7 +2913,7 @@ __global__ __launch_bounds__(256, (finish_waves<F, PN, LSM>())) void k_finish(co
             v3 L;
             bool cont = false;
             if (leaf < 0) L = sky_radiance(sc, p.d);
-            else cont = shade_hit<-1, PN, LSM, (F & kFeatCurves) != 0>(sc, P, rp, p, t, leaf, L, sc.leaves);
+            else cont = shade_hit<-1, PN, LSM, EX>(sc, P, rp, p, t, leaf, L, sc.leaves);
             if (!cont) { write_sample(rp, p, L); active = false; }
         }
     }
@@ -3061,11 +3125,11 @@ hipError_t launch_shade(int mat, const DevScene& sc, const DevScene* scd, const 
             hipLaunchKernelGGL((k_shade<M, PN, LS, false, EX>), dim3(blocks), dim3(256), lds, s, scd, rp, in,  \
                                hq, qv, out, out_counts, shard_cap, depth);                                   \
     } while (0)
-    // libm's own sin / cos for the bounce directions in scenes with curves (bounce_cos_sin); only the
-    // lambertian kernels draw directions with them
+    // libm's own sin / cos for the bounce directions (bounce_cos_sin: RT_OPT_EXACT_LIBM, by default in
+    // scenes with curves); only the lambertian kernels draw directions with them
 #define RT_SHADE(M, PN, LS)                                                                                  \
     do {                                                                                                     \
-        if (M == MAT_LAMBERTIAN && sc.n_bez > 0) RT_SHADE_EX(M, PN, LS, true);                              \
+        if (M == MAT_LAMBERTIAN && rp.exact_libm) RT_SHADE_EX(M, PN, LS, true);                             \
         else RT_SHADE_EX(M, PN, LS, false);                                                                  \
     } while (0)
     const bool pn = sc.has_noise_tex != 0;
@@ -3103,13 +3167,17 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
     if (tree0_lds) lds += solo ? tree - (size_t)sc.n_fbleaf * sizeof(BvhLeaf) : tree;
     // the Perlin tables ride at the end of the dynamic LDS, only where they are staged (PN and tables given)
     const size_t perlin = sc.has_perlin ? sizeof(PerlinLds) : 0;
+    // the bounce directions' sin / cos (RT_OPT_EXACT_LIBM): rt_libm.h's or the device library's
+    const bool ex = rp.exact_libm != 0;
 #define RT_FINISH_F(F) RT_FINISH(F, true, true)
-#define RT_FINISH_SOLO(PN, LS) \
-    hipLaunchKernelGGL((k_finish<0, PN, LS, true>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, in, \
-                       n, seg_count, tree0_lds, depth)
-#define RT_FINISH(F, PN, LS) \
-    hipLaunchKernelGGL((k_finish<F, PN, LS>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, in, n, \
-                       seg_count, tree0_lds, depth)
+#define RT_FINISH_SOLO_EX(PN, LS, EX) \
+    hipLaunchKernelGGL((k_finish<0, PN, LS, true, EX>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, \
+                       in, n, seg_count, tree0_lds, depth)
+#define RT_FINISH_EX(F, PN, LS, EX) \
+    hipLaunchKernelGGL((k_finish<F, PN, LS, false, EX>), dim3(blocks), dim3(256), lds + (PN ? perlin : 0), s, scd, rp, st, \
+                       in, n, seg_count, tree0_lds, depth)
+#define RT_FINISH_SOLO(PN, LS) do { if (ex) RT_FINISH_SOLO_EX(PN, LS, true); else RT_FINISH_SOLO_EX(PN, LS, false); } while (0)
+#define RT_FINISH(F, PN, LS) do { if (ex) RT_FINISH_EX(F, PN, LS, true); else RT_FINISH_EX(F, PN, LS, false); } while (0)
     // the plain-sphere feature set also gets Perlin / light-mixture specialisations:
     // the tail kernel carries every material's code, so dropping the unused ones
     // trims its register file
@@ -3130,6 +3198,8 @@ hipError_t launch_finish(const DevScene& sc, const DevScene* scd, const RenderPa
 #undef RT_FINISH_F
 #undef RT_FINISH_SOLO
 #undef RT_FINISH
+#undef RT_FINISH_SOLO_EX
+#undef RT_FINISH_EX
     return hipGetLastError();
 }
 // test hooks (render_impl: RTAMD_REJECT_CAP / RTAMD_CURVE_RAY_CAP, tests only): the samplers' attempt
@@ -3184,6 +3254,37 @@ extern "C" int rt_debug_stats(unsigned long long* out, int reset) {
 hipError_t launch_accumulate(const RenderParams& rp, uint32_t S, double* accum, hipStream_t s) {
     const uint32_t blocks = (rp.npix + 255u) / 256u;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks), dim3(256), 0, s, rp, S, accum);
+    return hipGetLastError();
+}
+// rt_curve_depth_probe: bez_maxd — the depth estimate every curve kernel runs (stage A, the per-lane
+// walk) — on caller-given ray-space control points (12 doubles per curve) and 8 eps
+__global__ __launch_bounds__(256) void k_curve_depth(const double* __restrict__ cps, const double* __restrict__ eps8,
+                                                     uint32_t n, int32_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= n) return;
+    const double* p = cps + 12 * (size_t)k;
+    Bez4 c;
+    c.p0 = mk(p[0], p[1], p[2]); c.p1 = mk(p[3], p[4], p[5]); c.p2 = mk(p[6], p[7], p[8]); c.p3 = mk(p[9], p[10], p[11]);
+    out[k] = bez_maxd(c, eps8[k]);
+}
+hipError_t launch_curve_depth(const double* cps, const double* eps8, uint32_t n, int32_t* out, hipStream_t s) {
+    if (n == 0u) return hipSuccess;
+    hipLaunchKernelGGL(k_curve_depth, dim3((n + 255u) / 256u), dim3(256), 0, s, cps, eps8, n, out);
+    return hipGetLastError();
+}
+// the frame-end gather's placement (rt_gather_shards): shard pixel q's three sums to image pixel pix[q]
+__global__ __launch_bounds__(256) void k_scatter_pixels(const double* __restrict__ src, const uint32_t* __restrict__ pix,
+                                                        uint32_t n, double* __restrict__ frame) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= n) return;
+    const size_t j = pix[q];
+    frame[3 * j] = src[3 * (size_t)q];
+    frame[3 * j + 1] = src[3 * (size_t)q + 1];
+    frame[3 * j + 2] = src[3 * (size_t)q + 2];
+}
+hipError_t launch_scatter_pixels(const double* src, const uint32_t* pix, uint32_t n, double* frame, hipStream_t s) {
+    if (n == 0u) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_pixels, dim3((n + 255u) / 256u), dim3(256), 0, s, src, pix, n, frame);
     return hipGetLastError();
 }
 hipError_t launch_resolve_u8(const double* accum, uint32_t n, int count, uint8_t* out, hipStream_t s) {

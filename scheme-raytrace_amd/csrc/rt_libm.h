@@ -20,11 +20,13 @@
 // Checked on the host against the C library bit for bit
 // (tests/csrc/libm_check.cpp, tests/test_libm.py: 0 differences over 2e7
 // random arguments, the random-cosine-direction angles 2 pi u included).
-// Valid for |x| < 105414350, the reference algorithm's fast reduction range
-// (beyond it glibc switches to a Payne-Hanek reduction this file does not
-// restate; no argument on the path comes near: the angles lie in (0, 2 pi),
-// marble's sin(scale z + 10 turb) in the scene's scale).  The table may be
-// passed in: the shade kernels stage a copy in LDS (rt_kernels.hip).
+// sin_ / cos_ are valid for |x| < 0x1.921fbp+26, the reference algorithm's fast
+// reduction range (beyond it glibc switches to a Payne-Hanek reduction this
+// file does not restate); sin_full / cos_full / sincos_full take every
+// argument and fall back to the platform's function outside that range (the
+// bounce angles lie in (0, 2 pi), but marble's sin(scale z + 10 turb) follows
+// the scene's scale).  The table may be passed in: the shade kernels stage a
+// copy in LDS (rt_kernels.hip).
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -228,7 +230,7 @@ RT_LIBM_FN uint32_t hiword(const double x) { return (uint32_t)(bits(x) >> 32) & 
 
 RT_LIBM_FN bool in_range(const double x) { return hiword(x) < 0x419921FBu; }
 
-// sin (cos_ = false) or cos (true) of x, |x| < 105414350 (in_range).  The
+// sin (cos_ = false) or cos (true) of x, |x| < 0x1.921fbp+26 (in_range).  The
 // reference's range cases — |x| < 0.855469: the kernel on x itself; up to
 // 2.426265: the other kernel on pi/2 - |x| (as a double-double); beyond: the
 // kernel picked by the quadrant of the four-part reduction — all come down to
@@ -263,5 +265,15 @@ RT_LIBM_FN double sincos_(const double x, const bool want_cos, const double* tab
 }
 RT_LIBM_FN double sin_(const double x) { return sincos_(x, false); }
 RT_LIBM_FN double cos_(const double x) { return sincos_(x, true); }
+
+// Every argument: the restatement inside its reduction range; beyond it (|x| >= 0x1.921fbp+26, where the
+// reference algorithm switches to its Payne-Hanek reduction, and inf / nan) the platform's own function
+// — the device library on the GPU (within 1 ulp), the C library itself on the host.
+RT_LIBM_FN double sincos_full(const double x, const bool want_cos, const double* tab = kSinCosTab) {
+    if (in_range(x)) return sincos_(x, want_cos, tab);
+    return want_cos ? ::cos(x) : ::sin(x);
+}
+RT_LIBM_FN double sin_full(const double x) { return sincos_full(x, false); }
+RT_LIBM_FN double cos_full(const double x) { return sincos_full(x, true); }
 
 }  // namespace rtlibm

@@ -21,7 +21,11 @@ RT_CAMERA_DOUBLES = 24
 RT_SKY_GRADIENT, RT_SKY_BLACK = 0, 1
 RT_RECT_XY, RT_RECT_XZ, RT_RECT_YZ = 0, 1, 2
 #: render-schedule options of a context (include/rt.h RT_OPT_*; 0 = automatic)
-RT_OPTIONS = {"lanes": 1, "max_paths": 2, "tail_paths": 3, "tail_div": 4, "tail_off": 5}
+RT_OPTIONS = {"lanes": 1, "max_paths": 2, "tail_paths": 3, "tail_div": 4, "tail_off": 5, "exact_libm": 6}
+#: RT_OPT_EXACT_LIBM values: auto (exact in scenes with curves), exact (the C library's sin / cos bit for
+#: bit), device (the device library's)
+RT_LIBM = {"auto": 0, "exact": 1, "device": 2}
+RT_COMM_ID_BYTES = 128
 
 
 class RtStats(ctypes.Structure):
@@ -52,7 +56,8 @@ class RtSceneInfo(ctypes.Structure):
                                               "bvh_solo")] + \
                [(n, ctypes.c_uint32) for n in ("extend_lds_bytes", "extend_lds_blocks", "camera_lds_bytes",
                                                "camera_lds_blocks")] + \
-               [("cus", ctypes.c_int32), ("curve_stack", ctypes.c_int32)]
+               [("cus", ctypes.c_int32), ("curve_stack", ctypes.c_int32), ("commit_ms", ctypes.c_double),
+                ("commit_upload_ms", ctypes.c_double)]
 
 
 # name -> argtypes (restype is always c_int status, except where noted)
@@ -120,6 +125,11 @@ _SIGNATURES = {
                         ctypes.POINTER(ctypes.c_int64)],
     "rt_resolve_u8_device": [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p],
+    "rt_curve_depth_probe": [ctypes.c_int, ctypes.c_int, _c_double_p, _c_double_p, _c_i32_p],
+    "rt_comm_unique_id": [ctypes.POINTER(ctypes.c_uint8)],
+    "rt_comm_create": [ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int, _c_int_p],
+    "rt_comm_destroy": [ctypes.c_int],
+    "rt_gather_shards": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
 }
 
 #: every symbol include/rt.h declares (tests check the .so exports all of them)

@@ -13,7 +13,12 @@ summed).
 
 ``gather_frame`` is the exchange step; bench.py calls it after each rank's
 rt_render_shard_device (timing the two apart), tests/test_distributed.py calls
-it with gloo on CPU tensors.
+it with gloo on CPU tensors.  On GPUs ("nccl" backend) it runs behind the C
+ABI: rt_gather_shards over a librtamd communicator (rt_comm_create, its id
+made by rank 0 and broadcast over the process group), which sends each
+shard's exact pixel count (grouped send / receive, no padding) and places the
+pixels into rank 0's frame on the device; the gloo path (CPU rehearsals) is
+the same exchange in torch.distributed.
 """
 import numpy as np
 
@@ -21,6 +26,7 @@ from . import gpu
 
 _pix_cache = {}
 _dev_cache = {}
+_comms = {}
 
 
 def shard_pixels(nx, ny, world):
@@ -66,9 +72,17 @@ def gather_frame(local, nx, ny, rank, world, group=None, out=None):
     counts = [len(p) for p in pix]
     if local.numel() != 3 * counts[rank]:
         raise ValueError("rank %d holds %d values, its shard has %d pixels" % (rank, local.numel(), counts[rank]))
-    # RCCL gathers device buffers; gloo (CPU tests, one-GPU rehearsals of the
-    # multi-process bench) gathers host copies
-    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else local.device
+    if dist.get_backend(group) != "gloo":          # GPUs: the C ABI's RCCL gather (rt_gather_shards)
+        if rank == 0 and out is None:
+            out = torch.empty(nx * ny * 3, dtype=local.dtype, device=local.device)
+        if rank == 0 and out.numel() != nx * ny * 3:
+            raise ValueError("out must hold nx*ny*3 values")
+        comm = communicator(rank, world, group, local.device)
+        comm.gather_shards(nx, ny, local.data_ptr(), out.data_ptr() if rank == 0 else 0,
+                           torch.cuda.current_stream(local.device).cuda_stream)
+        return out if rank == 0 else None
+    # gloo (CPU tests, one-GPU rehearsals of the multi-process bench) gathers host copies
+    dev = torch.device("cpu")
     B = _gather_buffers(nx, ny, world, local.dtype, dev, local.device)
     send = B["send"]
     send[:local.numel()].copy_(local)
@@ -84,6 +98,23 @@ def gather_frame(local, nx, ny, rank, world, group=None, out=None):
     recv = B["recv"].to(local.device).view(-1, 3)     # the shards cover every pixel exactly once
     out.view(-1, 3).index_copy_(0, B["dst"], recv.index_select(0, B["src"]))
     return out
+
+
+def communicator(rank, world, group=None, device=None):
+    """The process's librtamd communicator for `group` (rt_comm_create), made once: rank 0's
+    rt_comm_unique_id is broadcast over the group, then every rank joins."""
+    import torch
+    import torch.distributed as dist
+    key = (id(group), rank, world)
+    if key not in _comms:
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        buf = torch.zeros(gpu._lib.RT_COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            buf.copy_(torch.frombuffer(bytearray(gpu.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(buf, src=0, group=group)
+        ctx = gpu.default_context(dev.index if getattr(dev, "index", None) is not None else 0)
+        _comms[key] = gpu.Comm(bytes(buf.cpu().numpy().tobytes()), rank, world, ctx=ctx)
+    return _comms[key]
 
 
 def render_frame(scene, nx, ny, spp_begin, spp_count, seed, rank, world, local=None, frame=None, stream=None,

@@ -24,7 +24,11 @@ class Context:
     def set_option(self, name, value):
         """rt_context_set_option: a render-schedule option (_lib.RT_OPTIONS:
         lanes, max_paths, tail_paths, tail_div, tail_off); 0 = automatic.
-        No option changes an image, only how the work is scheduled."""
+        No schedule option changes an image, only how the work is scheduled.
+        exact_libm (value or a _lib.RT_LIBM name: auto / exact / device)
+        selects the bounce directions' sin / cos."""
+        if name == "exact_libm" and isinstance(value, str):
+            value = _lib.RT_LIBM[value]
         call("rt_context_set_option", self.handle, _lib.RT_OPTIONS[name], int(value))
 
     def get_option(self, name):
@@ -288,6 +292,58 @@ def resolve_u8_device(accum_ptr, nx, ny, sample_count, out_ptr, stream=None, ctx
     ctx = ctx or default_context()
     call("rt_resolve_u8_device", ctx.handle, ctypes.c_void_p(accum_ptr), nx, ny, int(sample_count),
          ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or 0))
+
+
+def curve_depth_probe(cps, eps8, ctx=None):
+    """rt_curve_depth_probe: the curve kernels' depth estimate (bez_maxd) for ray-space control points
+    cps (n, 12) and 8 eps (n,); returns int32 depths."""
+    ctx = ctx or default_context()
+    c = np.ascontiguousarray(cps, dtype=np.float64).reshape(-1, 12)
+    e = np.ascontiguousarray(eps8, dtype=np.float64).ravel()
+    if e.size != c.shape[0]:
+        raise ValueError("one eps8 per curve")
+    out = np.zeros(c.shape[0], dtype=np.int32)
+    call("rt_curve_depth_probe", ctx.handle, c.shape[0], c.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+         e.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def comm_unique_id():
+    """rt_comm_unique_id: a new communicator id (RT_COMM_ID_BYTES bytes), made by rank 0."""
+    buf = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES)()
+    call("rt_comm_unique_id", buf)
+    return bytes(buf)
+
+
+class Comm:
+    """rt_comm_create / rt_gather_shards / rt_comm_destroy: the frame-end gather of a multi-GPU frame
+    (one process per GPU) over RCCL, behind the C ABI."""
+
+    def __init__(self, unique_id, rank, world, ctx=None):
+        if len(unique_id) != _lib.RT_COMM_ID_BYTES:
+            raise ValueError("a communicator id has %d bytes" % _lib.RT_COMM_ID_BYTES)
+        self.ctx = ctx or default_context()
+        self.rank, self.world = rank, world
+        buf = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        h = ctypes.c_int(0)
+        call("rt_comm_create", self.ctx.handle, buf, rank, world, ctypes.byref(h))
+        self.handle = h.value
+
+    def gather_shards(self, nx, ny, accum_compact_ptr, frame_ptr, stream=None):
+        """rt_gather_shards (collective): every rank's compact accumulator into rank 0's frame."""
+        call("rt_gather_shards", self.handle, nx, ny, ctypes.c_void_p(accum_compact_ptr),
+             ctypes.c_void_p(frame_ptr or 0), ctypes.c_void_p(stream or 0))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            call("rt_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def shard_pixels(nx, ny, shard, nshard):

@@ -133,8 +133,10 @@ def make_bezier(a, b, c, d, width, material):
     width.  Its hit t is a distance along unit(dir) used as a parameter of the
     raw ray (Q10) and its normal is -dir (Q12); see DESIGN.md."""
     _need(material, Material, "make-bezier material")
-    if not float(width) > 0.0:
-        raise ValueError("make-bezier: width must be positive")
+    w = float(width)
+    if not (w == w and abs(w) != float("inf") and w != 0.0):
+        # the reference accepts any width; zero would divide by zero in the depth estimate (eps = width/20)
+        raise ValueError("make-bezier: width must be finite and nonzero (negative widths as the reference)")
     return Hitable("bezier", v.vec3(*a), v.vec3(*b), v.vec3(*c), v.vec3(*d), float(width), material)
 
 
@@ -144,8 +146,9 @@ def bezier_array(cps, width, material):
     one width and material.  Behaves as the list of those curves."""
     import numpy as np
     _need(material, Material, "bezier->objs material")
-    if not float(width) > 0.0:
-        raise ValueError("bezier->objs: width must be positive")
+    w = float(width)
+    if not (w == w and abs(w) != float("inf") and w != 0.0):
+        raise ValueError("bezier->objs: width must be finite and nonzero")
     arr = np.ascontiguousarray(cps, dtype=np.float64)
     if arr.ndim != 2 or arr.shape[1] != 12:
         raise ValueError("bezier->objs: control points must have shape (n, 12)")

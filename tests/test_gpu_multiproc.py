@@ -4,8 +4,9 @@ interleaved tiles with librtamd (rt_render_shard_device, compact accumulator)
 through rtamd.dist.render_frame — bench.py's per-step call — and rank 0's
 gathered frame must equal a one-process rt_render_device frame bit for bit.
 Only the transport differs from the 8-GPU bench (gloo through host memory
-instead of RCCL over xGMI); the RCCL path itself runs at world size 1
-(test_rccl_gather_world1_equals_render_device)."""
+instead of RCCL over xGMI); the RCCL path itself — rt_gather_shards behind
+the C ABI — runs at world size 1 (test_rccl_gather_world1_equals_render_device,
+test_capi_gather_shards_world1)."""
 import os
 import socket
 
@@ -73,8 +74,10 @@ def _nccl_worker(rank, world, port, out_path):
     """RCCL ("nccl" backend) at world size 1 on cuda:0 — the only RCCL
     configuration a one-GPU box can run: the rank renders its (only) shard
     into a compact device accumulator and rtamd.dist.gather_frame moves it
-    with dist.gather over RCCL into a device frame, twice (the second frame
-    reuses the cached exchange buffers)."""
+    over RCCL into a device frame — through the C ABI since round 5
+    (rt_comm_create with the id broadcast over the process group, then
+    rt_gather_shards) — twice (the second frame reuses the communicator and
+    the cached pixel lists)."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "scheme-raytrace_amd"))
@@ -117,6 +120,30 @@ def test_rccl_gather_world1_equals_render_device(sched, tmp_path):
     gpu.render_device(scenes.random_scene(NX, NY), NX, NY, 0, SPP, SEED, full.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(np.load(out), full.cpu().numpy())
+
+
+def test_capi_gather_shards_world1(sched):
+    """The frame-end gather behind the C ABI alone (rt_comm_unique_id, rt_comm_create, rt_gather_shards,
+    rt_comm_destroy — what a Scheme or C host calls), without torch.distributed: world size 1, the rank's
+    compact accumulator into a device frame, bitwise equal to rt_render_device; two frame sizes on one
+    communicator (the pixel lists are rebuilt when the size changes)."""
+    import torch
+    from rtamd import dist as rdist
+    from rtamd import gpu, scenes
+    comm = gpu.Comm(gpu.comm_unique_id(), 0, 1, ctx=sched)
+    try:
+        for nx, ny in ((NX, NY), (53, 37)):
+            scene = scenes.random_scene(nx, ny)
+            full = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+            gpu.render_device(scene, nx, ny, 0, SPP, SEED, full.data_ptr(), ctx=sched)
+            local = torch.zeros(rdist.local_size(nx, ny, 0, 1), dtype=torch.float64, device="cuda")
+            gpu.render_shard_device(scene, nx, ny, 0, SPP, SEED, 0, 1, local.data_ptr(), ctx=sched)
+            frame = torch.full((nx * ny * 3,), -1.0, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            comm.gather_shards(nx, ny, local.data_ptr(), frame.data_ptr())
+            assert torch.equal(frame, full)
+    finally:
+        comm.close()
 
 
 def test_bench_two_ranks_self_verifying(tmp_path):

@@ -429,6 +429,10 @@ def test_c_example_matches_python_host(sched, tmp_path):
     ppm_py = tmp_path / "py.ppm"
     render.write_ppm(str(ppm_py), gpu.resolve_u8(acc, nx, ny, spp), nx, ny)
     assert ppm_c.read_bytes() == ppm_py.read_bytes()
+    # the multi-GPU frame's path from C at world size 1: rt_render_shard_device + rt_gather_shards
+    ppm_g = tmp_path / "g.ppm"
+    subprocess.run([str(exe), str(nx), str(ny), str(spp), str(ppm_g), "gather"], check=True, timeout=300)
+    assert ppm_g.read_bytes() == ppm_py.read_bytes()
 
 
 _WAVEFRONT_SCENES = ["cover", "cover_marble", "test_scene2", "cornell", "cornell_mixture", "cornell_smoke",

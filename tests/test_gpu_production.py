@@ -34,12 +34,14 @@ def _compare(a, b, n):
 
 @pytest.fixture(scope="module")
 def c2_band(gpu_ctx, oracle_mod):
-    """Config C2 (cover scene, 1920x1080) rows 400..415, passes 1000..1023,
+    """Config C2 (cover scene, 1920x1080) rows 528..543, passes 1000..1023,
     through the production schedule: 8 chunks of 3 passes (92 160 paths each,
-    above the tail threshold) on 2 lanes.  Returns the GPU accumulator, the
+    above the tail threshold) on 2 lanes.  The rows cross the horizon, where
+    grazing bounces off the ground concentrate the device library's sin / cos
+    ulps (test_horizon_rows_exact_libm).  Returns the GPU accumulator, the
     oracle's, and the render statistics."""
     import torch
-    nx, ny, y0, rows, s0, n = 1920, 1080, 400, 16, 1000, 24
+    nx, ny, y0, rows, s0, n = 1920, 1080, 528, 16, 1000, 24
     scene = scenes.random_scene(nx, ny)
     with gpu_ctx.options(max_paths=3 * rows * nx, lanes=2):
         acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
@@ -122,6 +124,48 @@ def test_config_band_production_vs_oracle(sched, oracle_mod, name):
     assert rms <= RMS_TOL
     assert nbad <= max(2, npx // 200)
     assert not got[:3 * lo].any() and not got[3 * hi:].any()
+
+
+@pytest.mark.parametrize("name", ["cover", "cover_marble"])
+def test_horizon_rows_exact_libm(sched, oracle_mod, name):
+    """C2 / C3 frame rows 536..543 (the horizon band of the 1920x1080 frame, where the bench's parity_frame
+    rows sit), passes 0..63, production schedule (8 chunks on 2 lanes).  With RT_OPT_EXACT_LIBM = exact
+    the bounce directions' sin / cos are the C library's bit for bit, and the image must equal the oracle's
+    to the last bits: 0 pixels off by more than 1e-9.  The default mode (the device library's sin / cos in
+    scenes without curves) is rendered too, and its count printed."""
+    import torch
+    nx, ny, y0, rows, n = 1920, 1080, 536, 8, 64
+    scene = scenes.SCENES[name](nx, ny)
+    lo, hi = y0 * nx, (y0 + rows) * nx
+    ref = np.zeros(nx * ny * 3)
+    oracle_mod.build_scene(scene).render(nx, ny, 0, n, SEED, ref, lo, hi, nthreads=host_threads())
+    sched.set_option("max_paths", 8 * rows * nx)
+    sched.set_option("lanes", 2)
+    res = {}
+    for mode in ("exact", "auto"):
+        sched.set_option("exact_libm", mode)
+        acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+        h = gpu.render_rows_device(scene, nx, ny, y0, rows, 0, n, SEED, acc.data_ptr())
+        st = gpu.stats(h)
+        assert st.chunks >= 4 and st.lanes == 2 and st.extend_rays > st.paths
+        res[mode] = _compare(acc.cpu().numpy()[3 * lo:3 * hi], ref[3 * lo:3 * hi], n)
+        print("%s rows %d..%d passes 0..%d, exact_libm=%s: rms=%.3e max=%.3e pixels>1e-9: %d/%d"
+              % (name, y0, y0 + rows - 1, n - 1, mode, *res[mode]))
+    rms, dmax, nbad, npx = res["exact"]
+    assert nbad == 0 and rms <= 1e-12, res["exact"]
+    assert res["auto"][0] <= RMS_TOL
+
+
+def test_exact_libm_option_values(sched):
+    """RT_OPT_EXACT_LIBM takes auto / exact / device (0 / 1 / 2) and refuses anything else; the
+    schedule options do not touch it."""
+    from rtamd._lib import RtError
+    assert sched.get_option("exact_libm") == 0
+    for mode, v in (("exact", 1), ("device", 2), ("auto", 0)):
+        sched.set_option("exact_libm", mode)
+        assert sched.get_option("exact_libm") == v
+    with pytest.raises(RtError, match="RT_OPT_EXACT_LIBM"):
+        sched.set_option("exact_libm", 3)
 
 
 def test_trace_line_row_by_row_equals_trace_all(gpu_ctx):
@@ -285,6 +329,32 @@ def test_pools_shared_per_context_and_released(gpu_ctx, monkeypatch):
             ctx.release_pools()
         assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[1], outs[3])
         assert not np.array_equal(outs[0], outs[1])
+    finally:
+        ctx.close()
+
+
+def test_raising_lanes_resizes_pools():
+    """The path pools are sized at a render so that the lanes together take at most 55 % of the free
+    device memory.  Raising RT_OPT_LANES afterwards (2 -> 4) must size them again for four lanes (round-4
+    advice: each extra lane used to allocate another pool of the two-lane size, ~110 % of the budget),
+    and the image must not change."""
+    import torch
+    from rtamd.gpu import Context
+    ctx = Context(0)
+    try:
+        nx, ny, spp = 1920, 1080, 600             # > 4 chunks of the largest pools, so four lanes run
+        sc = scenes.random_scene(nx, ny)
+        out = []
+        for lanes in (2, 4):
+            ctx.set_option("lanes", lanes)
+            acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+            h = gpu.render_device(sc, nx, ny, 0, spp, SEED, acc.data_ptr(), ctx=ctx)
+            st = gpu.stats(h)
+            torch.cuda.synchronize()
+            print("lanes %d: chunks %d, lanes used %d" % (lanes, st.chunks, st.lanes))
+            assert st.lanes == lanes
+            out.append(acc)
+        assert torch.equal(out[0], out[1])
     finally:
         ctx.close()
 

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_errors_without_gpu():
     L = _lib.lib()
-    assert L.rt_abi_version() == 5
+    assert L.rt_abi_version() == 6
     h = ctypes.c_int(0)
     assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
     assert b"invalid context" in L.rt_last_error()
@@ -181,9 +181,10 @@ def _build_c_example(tmp_path):
     import subprocess
     exe = tmp_path / "cornell"
     rtamd_dir = os.path.join(ROOT, "scheme-raytrace_amd", "rtamd")
-    subprocess.run(["gcc", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "examples", "cornell.c"), "-L", rtamd_dir, "-l:librtamd.so",
-                    "-Wl,-rpath," + rtamd_dir, "-o", str(exe)], check=True)
+    subprocess.run(["gcc", "-O2", "-Wall", "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "examples", "cornell.c"), "-L", rtamd_dir,
+                    "-l:librtamd.so", "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath," + rtamd_dir, "-o", str(exe)],
+                   check=True)
     return exe
 
 
@@ -192,7 +193,7 @@ def test_c_example_builds_against_the_abi(tmp_path):
     import subprocess
     exe = _build_c_example(tmp_path)
     out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
-    assert out.strip() == "rt_abi_version 5"
+    assert out.strip() == "rt_abi_version 6"
 
 
 def test_load_points_and_points_to_bezier(tmp_path):

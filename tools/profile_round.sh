@@ -7,9 +7,9 @@
 #        sq1:   VALUBusy VALUUtilization LdsUtil LdsBankConflict OccupancyPercent + SQ_WAIT_ANY SQ_INSTS_LDS
 #               SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES (+ GRBM_GUI_ACTIVE)
 #        sq2:   SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES + the f64 op counters + SQ_BUSY_CU_CYCLES
-#   3. tools/pmc_report.py -> profiles/pmc_round.json (per kernel family: bytes per item, VALU / LDS busy,
-#      lane utilisation, waits), and the extend / shade summaries bench.py reads (profiles/pmc_extend.json,
-#      profiles/pmc_shade.json)
+#   3. tools/pmc_report.py -> pmc_round.json in the output directory (per kernel family: bytes per item,
+#      VALU / LDS busy, lane utilisation, waits), and the extend / shade summaries bench.py reads
+#      (profiles/pmc/<scene>_{extend,shade}.json)
 # usage: tools/profile_round.sh TAG [extra bench args]
 set -e
 set -o pipefail
@@ -35,5 +35,5 @@ echo "sq1 ok"
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
   SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -f csv -d $O/sq2 -o s -- $P > $O/sq2.log 2>&1
 echo "sq2 ok"
-python3 tools/pmc_report.py $O $O/fetch.log profiles/pmc_round.json
-cp profiles/pmc_round.json profiles/pmc_extend.json profiles/pmc_shade.json $O/
+python3 tools/pmc_report.py $O $O/fetch.log $O/pmc_round.json
+cp profiles/pmc/*.json $O/
