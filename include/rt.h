@@ -118,8 +118,8 @@ int rt_add_moving_sphere(int scene, const double center0[3], const double center
 int rt_add_rect(int scene, int axis, double a0, double a1, double b0, double b1, double k,
                 int mat, int* out_obj);                                                          /* g:make-{xy,xz,yz}-rect :376-431 */
 /* cubic Bezier curve a,b,c,d of the given width (b:make-bezier bezier.scm:61); hit t is the distance
- * along unit(dir) and the normal is -dir (bezier.scm:176-214).  width: finite and nonzero (negative
- * widths behave as in the reference: converge's boxes shrink by |width|/2) */
+ * along unit(dir) and the normal is -dir (bezier.scm:176-214).  width: positive and finite (for width
+ * <= 0 the reference's depth estimate takes the log of a number <= 0 and raises on the first hit test) */
 int rt_add_bezier(int scene, const double a[3], const double b[3], const double c[3], const double d[3],
                   double width, int mat, int* out_obj);
 /* n curves at once (bezier->objs points.scm:45-53 over points->bezier output): cps holds n*12 doubles
@@ -176,7 +176,7 @@ int rt_scene_commit(int scene, int world_list_obj);
  * rt_render_device: accum is caller-owned DEVICE memory on the context's GPU
  * (e.g. a torch tensor's data_ptr); stream is a hipStream_t or NULL for the
  * context's own stream.  shard_index/shard_count select an interleaved subset
- * of 16x16 pixel tiles (tile t belongs to shard t % shard_count); pixels of
+ * of 16x16 pixel tiles (tile (tx, ty) belongs to shard (tx + 3 ty) % shard_count); pixels of
  * other shards are left untouched. */
 int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
               double* accum_host);
@@ -207,8 +207,9 @@ int rt_render_shard_device(int scene, int nx, int ny, int spp_begin, int spp_cou
                            int shard_index, int shard_count, double* accum_compact, void* stream);
 
 /* The pixels shard `shard_index` of `shard_count` renders (host-only, no GPU
- * needed): interleaved 16x16 tiles in row-major tile order, tile t belongs to
- * shard t % shard_count; pixel j = y*nx + x, listed tile by tile.  Pass
+ * needed): interleaved 16x16 tiles in row-major tile order, tile (tx, ty)
+ * belongs to shard (tx + 3 ty) % shard_count (diagonal, so no shard gets whole
+ * columns); pixel j = y*nx + x, listed tile by tile.  Pass
  * out_pix = NULL to get the count only. */
 int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* out_pix, int64_t* out_count);
 

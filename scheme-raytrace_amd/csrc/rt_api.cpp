@@ -1165,8 +1165,13 @@ std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
     const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
     std::vector<uint32_t> out;
     out.reserve((size_t)nx * (size_t)(ps.y1 - ps.y0) / (size_t)ps.nshard + T * T);
+    // tile (x, y) belongs to shard (x + 3 y) % nshard.  Plain t % nshard degenerates into vertical 16-px
+    // stripes whenever nshard divides the tiles per row (C2: 120, C4: 64): every rank then renders the same
+    // columns of every row, and the Cornell box's walls are not alike (shard balance at C4, one GPU per
+    // shard: max / mean 1.0385 for 8 shards, 1.0247 for 4; profiles/r05/balance.log).  The diagonal deal
+    // gives every shard one tile of each 8 consecutive ones along a row and along a column.
     for (int t = 0; t < tx * ty; ++t) {
-        if (t % ps.nshard != ps.shard) continue;
+        if (((t % tx) + 3 * (t / tx)) % ps.nshard != ps.shard) continue;
         const int bx = (t % tx) * T, by = (t / tx) * T;
         for (int yy = std::max(by, ps.y0); yy < std::min(std::min(by + T, ny), ps.y1); ++yy)
             for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
@@ -1766,9 +1771,11 @@ int rt_add_bezier(int scene, const double a[3], const double b[3], const double 
     OUT_OR_FAIL(out);
     if (!a || !b || !c || !d) return fail("rt_add_bezier: null control point");
     if (check_mat(s, mat)) return 1;
-    // any finite nonzero width, negative ones too (make-bezier has no check; width1 = width / 2 then
-    // shrinks converge's boxes and a hit needs |p.xy| < |width1|); zero would divide in the depth estimate
-    if (width == 0.0 || !std::isfinite(width)) return fail("rt_add_bezier: width must be finite and nonzero");
+    // make-bezier has no check, but a width <= 0 makes converge's depth estimate the log of a number
+    // <= 0 (eps = width / 20, bezier.scm:179-192): Gauche's log returns a complex (or -inf for 0) and
+    // ceiling->exact raises, so the reference fails on the first ray that tests such a curve
+    if (!(width > 0.0) || !std::isfinite(width))
+        return fail("rt_add_bezier: width must be positive and finite (the reference's depth estimate fails otherwise)");
     Obj o; o.type = O_BEZIER; o.mat = mat; o.width = width;
     const double* p[4] = {a, b, c, d};
     for (int i = 0; i < 4; ++i) for (int k = 0; k < 3; ++k) o.cp[3 * i + k] = p[i][k];
@@ -1779,9 +1786,11 @@ int rt_add_bezier_array(int scene, const double* cps, int n, double width, int m
     OUT_OR_FAIL(out_first);
     if (n < 0 || (n > 0 && !cps)) return fail("rt_add_bezier_array: invalid curve array");
     if (check_mat(s, mat)) return 1;
-    // any finite nonzero width, negative ones too (make-bezier has no check; width1 = width / 2 then
-    // shrinks converge's boxes and a hit needs |p.xy| < |width1|); zero would divide in the depth estimate
-    if (width == 0.0 || !std::isfinite(width)) return fail("rt_add_bezier_array: width must be finite and nonzero");
+    // make-bezier has no check, but a width <= 0 makes converge's depth estimate the log of a number
+    // <= 0 (eps = width / 20, bezier.scm:179-192): Gauche's log returns a complex (or -inf for 0) and
+    // ceiling->exact raises, so the reference fails on the first ray that tests such a curve
+    if (!(width > 0.0) || !std::isfinite(width))
+        return fail("rt_add_bezier_array: width must be positive and finite (the reference's depth estimate fails otherwise)");
     *out_first = (int)s->objs.size();
     s->objs.reserve(s->objs.size() + (size_t)n);
     for (int i = 0; i < n; ++i) {

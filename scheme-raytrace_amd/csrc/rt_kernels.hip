@@ -388,7 +388,7 @@ __device__ __forceinline__ bool bez_sep_axis(const Bez4& c, const v3 a, const v3
 __device__ __forceinline__ double bez_hull_r2(const Bez4& c, const double w1) {
     const double s = fmax(fmax(fmax(fabs(c.p0.x), fabs(c.p0.y)), fmax(fabs(c.p1.x), fabs(c.p1.y))),
                           fmax(fmax(fabs(c.p2.x), fabs(c.p2.y)), fmax(fabs(c.p3.x), fabs(c.p3.y))));
-    const double aw = fabs(w1);         // a hit needs |p.xy|^2 < width2 = w1^2: |w1| for a negative width too
+    const double aw = fabs(w1);         // a hit needs |p.xy|^2 < width2 = w1^2 (the ABI refuses widths <= 0)
     const double r = fma(aw, 1e-9, aw) + 1e-9 * s;
     return r * r;
 }

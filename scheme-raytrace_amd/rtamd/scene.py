@@ -134,9 +134,10 @@ def make_bezier(a, b, c, d, width, material):
     raw ray (Q10) and its normal is -dir (Q12); see DESIGN.md."""
     _need(material, Material, "make-bezier material")
     w = float(width)
-    if not (w == w and abs(w) != float("inf") and w != 0.0):
-        # the reference accepts any width; zero would divide by zero in the depth estimate (eps = width/20)
-        raise ValueError("make-bezier: width must be finite and nonzero (negative widths as the reference)")
+    if not (w > 0.0 and w != float("inf")):
+        # the reference has no check, but for width <= 0 converge's depth estimate takes the log of a
+        # number <= 0 (bezier.scm:179-192) and ceiling->exact raises on the first ray that tests the curve
+        raise ValueError("make-bezier: width must be positive and finite")
     return Hitable("bezier", v.vec3(*a), v.vec3(*b), v.vec3(*c), v.vec3(*d), float(width), material)
 
 
@@ -147,8 +148,8 @@ def bezier_array(cps, width, material):
     import numpy as np
     _need(material, Material, "bezier->objs material")
     w = float(width)
-    if not (w == w and abs(w) != float("inf") and w != 0.0):
-        raise ValueError("bezier->objs: width must be finite and nonzero")
+    if not (w > 0.0 and w != float("inf")):
+        raise ValueError("bezier->objs: width must be positive and finite")
     arr = np.ascontiguousarray(cps, dtype=np.float64)
     if arr.ndim != 2 or arr.shape[1] != 12:
         raise ValueError("bezier->objs: control points must have shape (n, 12)")

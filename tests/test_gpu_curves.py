@@ -297,41 +297,3 @@ def test_curve_hit_appends_spill_between_shards(sched, monkeypatch):
     print("one curve block, slack 256: paths %d, hits at depth 0 %d" % (st.paths, st.shade_hits_d0))
     assert st.shade_hits_d0 > st.paths // 4 + 8 * 256      # more hits than four unspilled shards could hold
     assert np.isfinite(a).all() and np.array_equal(a, b)
-
-
-def test_negative_width_curves_vs_oracle(sched, oracle_mod):
-    """b:make-bezier with a negative width (bezier.scm:61-66: width1 = width / 2 < 0, width2 = width1^2):
-    a hit needs |p.xy|^2 < width2, i.e. within |width1| of the ray.  The hull culls (not in the reference)
-    must bound with |width1| (round-4 advice: the signed width shrank their radius and could drop a hit);
-    the image against the oracle, and per ray against the oracle's closest hit."""
-    from rtamd import scene as gs
-    nx, ny, spp = 64, 48, 4
-    red = gs.make_lambertian(gs.constant_texture(v.vec3(0.65, 0.05, 0.05)))
-    white = gs.make_lambertian(gs.constant_texture(v.vec3(0.73, 0.73, 0.73)))
-    light = gs.make_diffuse_light(gs.constant_texture(v.vec3(7, 7, 7)))
-    rs = np.random.default_rng(11)
-    curves = []
-    for k in range(48):
-        p = rs.uniform([100, 50, 150], [450, 500, 450], size=(4, 3))
-        curves.append(gs.make_bezier(*[v.vec3(*q) for q in p], -float(rs.uniform(4, 12)), red))
-    objs = [gs.make_xz_rect(0, 555, 0, 555, 0, white), gs.flip_normals(gs.make_xz_rect(113, 443, 127, 432, 554,
-                                                                                           light)),
-            gs.make_bvh_node(curves, 0, 1)]
-    sc = gs.make_scene(objs, scenes.cornell_camera_for(nx, ny), gs.black)
-    _opts(sched, tail_off=1)
-    acc = np.zeros(nx * ny * 3)
-    gpu.render_host(sc, nx, ny, 0, spp, SEED, acc)
-    o = oracle_mod.build_scene(sc)
-    ref, _ = o.render(nx, ny, 0, spp, SEED, nthreads=host_threads())
-    rms, dmax, nbad, npx = _compare(acc, ref, spp)
-    print("negative-width curves: rms=%.3e max=%.3e pixels>1e-9: %d/%d" % (rms, dmax, nbad, npx))
-    assert np.isfinite(acc).all() and nbad == 0
-    cam_o = np.array([278.0, 278.0, -800.0])
-    tgt = rs.uniform([100, 50, 150], [450, 500, 450], size=(2048, 3))
-    rays = np.concatenate([np.tile(cam_o, (2048, 1)), tgt - cam_o, np.zeros((2048, 1))], axis=1)
-    t, m = gpu.hit_rays(sc, rays)
-    for k in range(len(rays)):
-        hh = o.hit_world(rays[k, 0:3], rays[k, 3:6])
-        et, em = (hh[0], int(hh[7])) if hh else (0.0, -1)
-        assert (et, em) == (t[k], m[k]), (k, et, em, t[k], m[k])
-    assert (m >= 0).sum() > 20

@@ -133,11 +133,11 @@ def test_shard_partition_is_exact(nx, ny, n):
     allpix = np.concatenate(parts)
     assert allpix.size == nx * ny
     assert np.array_equal(np.sort(allpix), np.arange(nx * ny, dtype=np.uint32))
-    # tile t -> shard t % n (16x16 tiles, row-major)
+    # tile (tx, ty) -> shard (tx + 3 ty) % n (16x16 tiles, row-major)
     tx = (nx + 15) // 16
     for r, p in enumerate(parts):
         x, y = p % nx, p // nx
-        assert np.all(((y // 16) * tx + x // 16) % n == r)
+        assert np.all((3 * (y // 16) + x // 16) % n == r)
 
 
 def test_resolve_matches_reference_formula(oracle_mod):
@@ -175,6 +175,19 @@ def test_medium_order_segments():
     assert [o.kind for o in sc.obj_list] == ["medium", "sphere"]
     with pytest.raises(ValueError):
         g.make_constant_medium(box, 0.0, g.constant_texture((1, 1, 1)))
+
+
+def test_curve_width_must_be_positive():
+    """make-bezier accepts any width in the reference, but for width <= 0 its depth estimate is the log of
+    a number <= 0 (bezier.scm:179-192): Gauche's log gives a complex number (or -inf) and ceiling->exact
+    raises on the first ray that tests the curve.  The host API and the C ABI refuse such widths up front."""
+    from rtamd import gpu  # noqa: F401
+    red = g.make_lambertian(g.constant_texture((0.65, 0.05, 0.05)))
+    for w in (0.0, -0.5, float("inf"), float("nan")):
+        with pytest.raises(ValueError):
+            g.make_bezier((0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0), w, red)
+        with pytest.raises(ValueError):
+            g.bezier_array(np.zeros((2, 12)), w, red)
 
 
 def _build_c_example(tmp_path):
