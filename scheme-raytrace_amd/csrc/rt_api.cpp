@@ -23,7 +23,7 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, hipStream_t);
+                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, const CurveSplit*, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t, hipStream_t);
 hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
@@ -98,6 +98,8 @@ constexpr int kLanes = 4;                  // most lanes a render may use (RT_OP
 constexpr int kCurveLdsStack = RT_CURVE_LDS_STACK;   // k_extend_curves' BVH4 stack entries in LDS per lane
 struct Lane {
     DevBuf st_a, st_b, hit, sb, counts, seg_tail;
+    DevBuf cw_buf;                             // the split curve extend's per-ray buffers (curve scenes)
+    CurveSplit cs{};
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
     hipStream_t stream = nullptr;
     hipEvent_t ev_cnt = nullptr;               // the last iteration's survivor counts are on the host
@@ -1042,6 +1044,7 @@ int commit_scene(Scene* s, int world) {
     }
     d.n_bleaf = (int)bleaf.size();
     d.lane_stack = lane_stack;
+    for (const BvhLeaf& L : bleaf) d.max_leaf_bez = std::max(d.max_leaf_bez, L.bn);
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (!bvh4.empty()) {
         if (int rc = upload(s->d_bvh4, bvh4, &d.bvh4)) return rc;
@@ -1211,14 +1214,59 @@ size_t max_paths(const Context& c, const int lanes) {
 int lanes_wanted(const Context& c) {   // RT_OPT_LANES: path pools kept in flight (1 = no overlap)
     return c.opt_lanes > 0 ? (int)std::min<int64_t>(c.opt_lanes, kLanes) : 2;
 }
+// The persistent curve kernels serve scenes whose world BVH holds every curve (launch_extend)
+bool curve_kernel_scene(const DevScene& d) {
+    return d.n_bez > 0 && d.bvh_has_bez && d.bez_groups == 0 && d.n_med == 0 && d.n_klein == 0;
+}
+// The split curve extend's per-ray buffers of a lane (rays per slice: at most 16M and the lane's pool):
+// closest 8 B, best 4, list length 4, K candidates of 8 B, the save area (S words), two continuation lists
+#ifndef RT_CURVE_K
+#define RT_CURVE_K 32
+#endif
+#ifndef RT_TRAV_LDS_STACK
+#define RT_TRAV_LDS_STACK 24           // k_curve_trav's LDS stack column (rt_kernels.hip, the same default)
+#endif
+constexpr int RT_TRAV_LDS_STACK_HOST = RT_TRAV_LDS_STACK;
+hipError_t ensure_curve_split(Lane& L, const DevScene& d, const size_t pool) {
+    // RTAMD_CURVE_K (tests): shorter lists, so rays continue over many rounds (k_curve_trav<true>)
+    const char* ke = std::getenv("RTAMD_CURVE_K");
+    const uint32_t K = (uint32_t)std::max(ke ? std::atoi(ke) : RT_CURVE_K, d.max_leaf_bez + 4);
+    const uint32_t S = (uint32_t)std::max(d.stack4, d.lds4) + 2u;
+    const uint32_t cap = (uint32_t)std::min<size_t>(pool, (size_t)16 << 20);
+    const size_t per = 8 + 4 + 4 + (size_t)K * 8 + (size_t)S * 4 + 2 * 4;
+    const char* le0 = std::getenv("RTAMD_CURVE_LDS_STACK");
+    const int lds = std::min(RT_TRAV_LDS_STACK_HOST, le0 ? std::max(1, std::atoi(le0)) : RT_TRAV_LDS_STACK_HOST);
+    if (L.cs.cap >= cap && L.cs.w.K == K && L.cs.w.S == S) { L.cs.w.lds = lds; return hipSuccess; }
+    const hipError_t e = L.cw_buf.ensure((size_t)cap * per + 2 * 256);
+    if (e != hipSuccess) return e;
+    char* p = L.cw_buf.as<char>();
+    CurveSplit cs{};
+    cs.w.closest = reinterpret_cast<double*>(p); p += (size_t)cap * 8;
+    cs.w.cand = reinterpret_cast<CurveCand*>(p); p += (size_t)cap * K * 8;
+    cs.w.best = reinterpret_cast<int32_t*>(p); p += (size_t)cap * 4;
+    cs.w.ncand = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
+    cs.w.save = reinterpret_cast<int32_t*>(p); p += (size_t)cap * S * 4;
+    cs.cont[0] = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
+    cs.cont[1] = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
+    cs.cnt[0] = reinterpret_cast<uint32_t*>(p); p += 256;
+    cs.cnt[1] = reinterpret_cast<uint32_t*>(p);
+    cs.w.K = K;
+    cs.w.S = S;
+    // RTAMD_CURVE_LDS_STACK (tests): fewer LDS entries, so the walk's deeper entries take the save area
+    const char* le = std::getenv("RTAMD_CURVE_LDS_STACK");
+    cs.w.lds = std::min(RT_TRAV_LDS_STACK_HOST, le ? std::max(1, std::atoi(le)) : RT_TRAV_LDS_STACK_HOST);
+    cs.cap = cap;
+    L.cs = cs;
+    return hipSuccess;
+}
+
 // Scenes whose world BVH holds curves run the persistent curve kernel, whose
 // grid fills the chip by itself: a second lane's kernels only queue behind it
 // and its narrow tails, so one lane is faster (C5 at 64 spp: 200.3 vs 164.1
 // Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RT_OPT_LANES overrides.
 int lanes_for(const Context& c, const DevScene& d) {
     if (c.opt_lanes > 0) return lanes_wanted(c);
-    const bool curve_kernel = d.n_bez > 0 && d.bvh_has_bez && d.bez_groups == 0 && d.n_med == 0 && d.n_klein == 0;
-    return curve_kernel ? 1 : lanes_wanted(c);
+    return curve_kernel_scene(d) ? 1 : lanes_wanted(c);
 }
 
 // A chunk's live paths at or below max(tail_threshold, B / tail_divisor) go to
@@ -1351,6 +1399,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(L.seg_tail.ensure(3 * sizeof(unsigned long long)));   // tail segments, next tail path, errors
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
+        if (curve_kernel_scene(s->dev)) HIPCHK(ensure_curve_split(L, s->dev, cap));
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
         HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 3 * sizeof(unsigned long long), L.stream));
         L.A = carve_state(L.st_a.p, scap);
@@ -1418,7 +1467,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             if (dl.bez_ring) dl.bez_ring += (size_t)L.index * dl.ring_waves * kBezRing * 16u;
             HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
-                                 reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1), L.stream));
+                                 reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1),
+                                 L.cs.cap ? &L.cs : nullptr, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
