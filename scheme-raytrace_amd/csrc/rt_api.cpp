@@ -39,6 +39,7 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
                              const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t launch_scatter_pixels(const double*, const uint32_t*, uint32_t, double*, hipStream_t);
+bool curve_split();
 hipError_t launch_curve_depth(const double*, const double*, uint32_t, int32_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
 hipError_t take_curve_stats(unsigned long long out[2]);
@@ -85,6 +86,11 @@ struct DevBuf {
         if (e == hipSuccess) bytes = n;
         return e;
     }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -94,6 +100,17 @@ struct DevBuf {
 // long, narrow tail of one chunk (its last few paths bouncing to depth 100)
 // overlaps the wide first iterations of the next one instead of leaving the
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
+#ifndef RT_CURVE_K
+#define RT_CURVE_K 32
+#endif
+#ifndef RT_TRAV_LDS_STACK
+#define RT_TRAV_LDS_STACK 24           // k_curve_trav's LDS stack column (rt_kernels.hip, the same default)
+#endif
+constexpr int RT_TRAV_LDS_STACK_HOST = RT_TRAV_LDS_STACK;
+#ifndef RT_CURVE_LIST_WAVES
+#define RT_CURVE_LIST_WAVES 2          // k_extend_curves<true>'s waves per SIMD (rt_kernels.hip, the same default)
+#endif
+constexpr int RT_CURVE_LIST_WAVES_HOST = RT_CURVE_LIST_WAVES;
 constexpr int kLanes = 4;                  // most lanes a render may use (RT_OPT_LANES)
 constexpr int kCurveLdsStack = RT_CURVE_LDS_STACK;   // k_extend_curves' BVH4 stack entries in LDS per lane
 struct Lane {
@@ -1060,7 +1077,7 @@ int commit_scene(Scene* s, int world) {
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
             HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * RT_CURVE_WAVES;
+            d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * (uint32_t)std::max(RT_CURVE_WAVES, RT_CURVE_LIST_WAVES_HOST);
             HIPCHK(s->d_bez_ring.ensure((size_t)kLanes * d.ring_waves * kBezRing * 128u));
             d.bez_ring = s->d_bez_ring.as<double>();
         }
@@ -1220,13 +1237,6 @@ bool curve_kernel_scene(const DevScene& d) {
 }
 // The split curve extend's per-ray buffers of a lane (rays per slice: at most 16M and the lane's pool):
 // closest 8 B, best 4, list length 4, K candidates of 8 B, the save area (S words), two continuation lists
-#ifndef RT_CURVE_K
-#define RT_CURVE_K 32
-#endif
-#ifndef RT_TRAV_LDS_STACK
-#define RT_TRAV_LDS_STACK 24           // k_curve_trav's LDS stack column (rt_kernels.hip, the same default)
-#endif
-constexpr int RT_TRAV_LDS_STACK_HOST = RT_TRAV_LDS_STACK;
 hipError_t ensure_curve_split(Lane& L, const DevScene& d, const size_t pool) {
     // RTAMD_CURVE_K (tests): shorter lists, so rays continue over many rounds (k_curve_trav<true>)
     const char* ke = std::getenv("RTAMD_CURVE_K");
@@ -1399,7 +1409,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
         HIPCHK(L.seg_tail.ensure(3 * sizeof(unsigned long long)));   // tail segments, next tail path, errors
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
-        if (curve_kernel_scene(s->dev)) HIPCHK(ensure_curve_split(L, s->dev, cap));
+        if (curve_kernel_scene(s->dev) && curve_split()) HIPCHK(ensure_curve_split(L, s->dev, cap));
+        else if (L.cs.cap) { L.cs = CurveSplit{}; L.cw_buf.release(); }   // (the previous render drained the lane)
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
         HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 3 * sizeof(unsigned long long), L.stream));
         L.A = carve_state(L.st_a.p, scap);

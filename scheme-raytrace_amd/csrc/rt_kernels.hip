@@ -730,7 +730,9 @@ static_assert(kBezS <= kBezRing && (kBezRing & (kBezRing - 1)) == 0,
               "k_extend_curves' survivor ring holds every survivor a wave can hold (slot = rtail + position)");
 static_assert(2 * 64 <= kBezQ, "stage B's donation handover: two words per donor lane in W.q");
 static_assert(kBezMaxDepth + 1 < 26, "the handover packs a level (6 bits) above a node index (26 bits)");
-struct BezWave {
+template <bool SLOT_>
+struct BezWaveT {
+    static constexpr bool SLOT = SLOT_;
     BezRay ray[64];                 // owner lane's ray-space matrix
     double cl[64];                  // owner's closest t when a batch runs
     double hz[64];                  // owner's best curve z from the batch
@@ -739,11 +741,10 @@ struct BezWave {
     uint32_t sv[kBezS];             // root-test survivors waiting for subdivision
     double sz[kBezS];               // their results (z or +inf)
     uint32_t done[64];              // persistent kernel: owner's candidates resolved so far
-#if RT_BEZ_SLOT
-    Bez4 pend[64];                  // stage B: each lane's latest pending right sibling (bez_walk_split)
-#endif
+    Bez4 pend[SLOT_ ? 64 : 1];      // stage B: each lane's latest pending right sibling (bez_walk_split)
     uint8_t lev[kBezS];             // survivors' subdivision leaf levels (stage A)
 };
+using BezWave = BezWaveT<RT_BEZ_SLOT != 0>;
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -756,8 +757,8 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 // the survivor list (svn entries already there).  Returns the new count.
 // Every active lane calls it with the same arguments.
 // TRACK (k_extend_curves): survivors also go to the wave's ring (slot rtail + position, mod kBezRing)
-template <bool TRACK = false>
-__device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, const uint32_t qn, uint32_t svn,
+template <bool TRACK = false, class WV = BezWave>
+__device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, WV& W, const uint32_t qn, uint32_t svn,
                                                 BezRoot* __restrict__ ring = nullptr, const uint32_t rtail = 0u) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
@@ -808,8 +809,8 @@ __device__ __forceinline__ uint32_t bez_stage_a(const DevScene& sc, BezWave& W, 
 // depth estimate is negative, bezier.scm:130,189-193).  One atomic per pass;
 // read and cleared by take_curve_stats.
 __device__ unsigned long long g_curve_stats[2];
-template <bool TRACK = false>
-__device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, const uint32_t nb, const uint32_t svn,
+template <bool TRACK = false, class WV = BezWave>
+__device__ __forceinline__ void bez_stage_b(const DevScene& sc, WV& W, const uint32_t nb, const uint32_t svn,
                                             const BezRoot* __restrict__ ring = nullptr, const uint32_t rtail = 0u) {
     const unsigned long long act = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(act), rank = lanes_below(act);
@@ -923,11 +924,11 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
             const unsigned long long cl1 = __builtin_amdgcn_s_memtime();
             n_clk_leaf += cl1 - cl0;
 #endif
-#if RT_BEZ_SLOT
-            if (busy && !at_leaf) over = bez_walk_node<true>(wk, &W.pend[threadIdx.x & 63u]);
-#else
-            if (busy && !at_leaf) over = bez_walk_node(wk);
-#endif
+            if constexpr (WV::SLOT) {
+                if (busy && !at_leaf) over = bez_walk_node<true>(wk, &W.pend[threadIdx.x & 63u]);
+            } else {
+                if (busy && !at_leaf) over = bez_walk_node(wk);
+            }
 #ifdef RT_STATS
             n_clk_node += __builtin_amdgcn_s_memtime() - cl1;
 #endif
@@ -990,7 +991,8 @@ __device__ __forceinline__ void bez_stage_b(const DevScene& sc, BezWave& W, cons
 // takes the hit on a tie with a sphere or rect; between two curves at the
 // same z the later one of the list (BezierRec::order) is the one the scan
 // keeps, whichever batch tested it first.
-__device__ __forceinline__ void bez_take_batch(const DevScene& sc, const BezWave& W, const uint32_t lane,
+template <class WV>
+__device__ __forceinline__ void bez_take_batch(const DevScene& sc, const WV& W, const uint32_t lane,
                                                const int32_t bz, double& closest, int32_t& best) {
     const double z = W.hz[lane];
     if (z == INFINITY || z > closest) return;
@@ -1899,6 +1901,17 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // =====================================================================
 static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK <= 160 * 1024 / RT_CURVE_WAVES,
               "k_extend_curves: RT_CURVE_WAVES blocks of BezWave state and LDS stack columns must fit a CU's LDS");
+// the LIST kernel (no traversal stack) may run more waves per SIMD: its wave state without the
+// pending-sibling slots (RT_CURVE_LIST_SLOT 0) fits three 4-wave blocks per CU
+#ifndef RT_CURVE_LIST_WAVES
+#define RT_CURVE_LIST_WAVES 2
+#endif
+#ifndef RT_CURVE_LIST_SLOT
+#define RT_CURVE_LIST_SLOT RT_BEZ_SLOT
+#endif
+template <bool LIST> using CurveWave = BezWaveT<LIST ? (RT_CURVE_LIST_SLOT != 0) : (RT_BEZ_SLOT != 0)>;
+static_assert(4 * sizeof(CurveWave<true>) <= 160 * 1024 / RT_CURVE_LIST_WAVES,
+              "k_extend_curves<true>: RT_CURVE_LIST_WAVES blocks of wave state must fit a CU's LDS");
 #ifndef RT_CURVE_PREFETCH
 #define RT_CURVE_PREFETCH 1            // load the lane's next BVH4 node one iteration ahead (32 VGPRs)
 #endif
@@ -1910,22 +1923,19 @@ static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK 
 // state (no node, no stack, no box ray).  A ray whose traversal stopped at the list's capacity is handed
 // back (closest, best) and continues in the next round (cw.cont_out).  k: slice-local ray index (the ray
 // queue's k0 + k), claimed in order, or through cw.list in continuation rounds.
-#ifndef RT_SPLIT_INFLIGHT
-#define RT_SPLIT_INFLIGHT 1000000      // LIST: most candidates a lane keeps queued and unresolved (pruning vs idling)
-#endif
 // RTAMD_CURVE_DEBUG (diagnostics): [0] candidates listed, [1] candidates tested (not skipped), [2] BVH4 nodes
 // visited by k_curve_trav, [3] rays listed (summed over rounds)
 __device__ unsigned long long g_split_dbg[4];
 __device__ int g_split_dbg_on;
 template <bool LIST>
-__global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
+__global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                        const bool depth0, unsigned int* __restrict__ claim,
                                                        const CurveWork cw, const uint32_t k0) {
     extern __shared__ uint32_t s_lstack[];          // per-lane BVH4 stack column, 256 x sc.lds4 (dynamic LDS; !LIST)
-    __shared__ BezWave s_bw[4];
-    BezWave& W = s_bw[threadIdx.x >> 6];
+    __shared__ CurveWave<LIST> s_bw[4];
+    CurveWave<LIST>& W = s_bw[threadIdx.x >> 6];
     uint32_t* lstk = s_lstack + threadIdx.x;
     const uint32_t stride = blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
@@ -2127,7 +2137,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
 #endif
         // 3. one BVH4 step (bvh_closest_curves over the collapsed tree): the node's hit children
         //    nearest first, the nearest entered, the others pushed
-        if (LIST && active && trav && pb >= pe && queued - W.done[lane] < (uint32_t)RT_SPLIT_INFLIGHT) {
+        if (LIST && active && trav && pb >= pe) {
             // the next candidate of the list: queued unless its box starts beyond the closest hit so far
             // (the tree walk's cull of that box: its entry t against f32_up(closest * tscale))
             const uint2 c = nxt;
@@ -2235,9 +2245,7 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
         }
         // 5. batches: root culls at 64 queued candidates, subdivisions in
         //    multiples of 64 (everything once no lane can add candidates)
-        // lanes that can still add candidates (LIST: not held by RT_SPLIT_INFLIGHT unresolved ones)
-        const bool more = __ballot(active && (pb < pe || (trav && (!LIST || queued - W.done[lane] <
-                                                                                 (uint32_t)RT_SPLIT_INFLIGHT)))) != 0ull;
+        const bool more = __ballot(active && (trav || pb < pe)) != 0ull;
 #if RT_BEZ_WAIT_FLUSH
         const bool press = __popcll(__ballot(active && !trav && pb >= pe && W.done[lane] != queued)) >= RT_BEZ_WAIT_FLUSH;
 #else
@@ -2435,175 +2443,6 @@ __global__ __launch_bounds__(256, RT_TRAV_WAVES) void k_curve_trav(const DevScen
         sv[0] = node;
         sv[1] = sp;
         for (int e = 0; e < min(sp, LDS); ++e) sv[2 + e] = (int32_t)lstk[e * 256];
-    }
-}
-
-// k_curve_trav's persistent form: lanes refill from the slice's ray list (one claim atomic per wave,
-// once RT_TRAV_REFILL lanes are idle) and take one node or leaf step per iteration, so a wave is not held
-// by its longest walk; the same walk, lists and save areas as k_curve_trav
-#ifndef RT_TRAV_REFILL
-#define RT_TRAV_REFILL 16
-#endif
-template <bool RESUME>
-__global__ __launch_bounds__(256, RT_TRAV_WAVES) void k_curve_trav_p(const DevScene sc, const PathState st, const QView in,
-                                                                     const uint32_t k0, const uint32_t n, const CurveWork cw,
-                                                                     const bool depth0, unsigned int* __restrict__ claim) {
-    __shared__ uint32_t s_stk[RT_TRAV_LDS_STACK * 256];
-    const int LDS = cw.lds;
-    constexpr int32_t kNone = INT32_MIN;
-    const uint32_t lane = threadIdx.x & 63u;
-    const QMap qm = qmap(in);
-    uint32_t* lstk = s_stk + threadIdx.x;
-    int gb = 0;
-    while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
-    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
-    const uint32_t K = cw.K;
-    const int scap = (int)cw.S - 2;
-    const uint32_t cap = 2u * (uint32_t)(sc.n_bvh4 + sc.n_bleaf) + 16u;
-    bool active = false, exhausted = false;
-    uint32_t k = 0, i = 0, nc = 0, it = 0, dbg_nodes = 0;
-    double closest = kTmax, tscale = 1.0;
-    int32_t best = -1, node = kNone;
-    int sp = 0;
-    BoxRayW br{};
-    for (;;) {
-        const unsigned long long idle = __ballot(!active);
-        if (idle != 0ull && !exhausted && (__popcll(idle) >= RT_TRAV_REFILL || idle == __ballot(1))) {
-            const uint32_t cnt = (uint32_t)__popcll(idle);
-            const int leader = __ffsll((long long)idle) - 1;
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(claim, cnt);
-            base = (uint32_t)__shfl((int)base, leader, 64);
-            if (base + cnt >= n) exhausted = true;
-            const uint32_t t = base + lanes_below(idle);
-            if (!active && t < n) {
-                k = RESUME ? cw.list[t] : t;
-                i = qphys(qm, k0 + k);
-                const RayRec R = st.ray[i];
-                const v3 o = mk(R.ox, R.oy, R.oz), d = mk(R.dx, R.dy, R.dz);
-                int32_t* sv = cw.save + (size_t)k * cw.S;
-                if constexpr (!RESUME) {
-                    const double tm = depth0 ? st.tm[i] : 0.0;
-                    closest = kTmax;
-                    best = -1;
-                    for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
-                    node = gb < sc.n_groups ? sc.bvh4_root : kNone;
-                    sp = 0;
-                } else {
-                    closest = cw.closest[k];
-                    best = cw.best[k];
-                    node = sv[0];
-                    sp = sv[1];
-                    for (int e = 0; e < min(sp, LDS); ++e) lstk[e * 256] = (uint32_t)sv[2 + e];
-                }
-                br = box_ray_w(o, d);
-                tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
-                nc = 0; it = 0; dbg_nodes = 0;
-                active = true;
-            }
-        }
-        if (__ballot(active) == 0ull) {
-            if (exhausted) break;
-            continue;
-        }
-        if (!active) continue;
-        int32_t* sv = cw.save + (size_t)k * cw.S;     // [0] next node, [1] stack depth, [2 + e] entry e
-        CurveCand* out = cw.cand + (size_t)k * K;
-        auto push = [&](const int32_t e) {
-            if (sp >= scap) { raise_fault(RT_FAULT_PATH); return; }
-            if (sp < LDS) lstk[sp * 256] = (uint32_t)e;
-            else sv[2 + sp] = e;
-            ++sp;
-        };
-        auto pop = [&]() -> int32_t {
-            if (sp == 0) return kNone;
-            --sp;
-            return sp < LDS ? (int32_t)lstk[sp * 256] : sv[2 + sp];
-        };
-        bool stop = false;                            // the list is full: the next round goes on from `node`
-        if (++it > cap) { raise_fault(RT_FAULT_PATH); node = kNone; }
-        else if (node >= 0) {
-            if (nc + 4u > K) stop = true;
-            else {
-                ++dbg_nodes;
-                const BvhNode4 N = sc.bvh4[node];
-                const float tcap = f32_up(closest * tscale);
-                float key[4];
-                int32_t ref[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float tx0 = fmaf(N.lo[0][j], br.ix, -br.lx), tx1 = fmaf(N.hi[0][j], br.ix, -br.hx);
-                    const float ty0 = fmaf(N.lo[1][j], br.iy, -br.ly), ty1 = fmaf(N.hi[1][j], br.iy, -br.hy);
-                    const float tz0 = fmaf(N.lo[2][j], br.iz, -br.lz), tz1 = fmaf(N.hi[2][j], br.iz, -br.hz);
-                    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
-                    key[j] = (tn <= tf && j < N.n) ? tn : INFINITY;
-                    ref[j] = N.ref[j];
-                }
-                auto cswap = [&](const int x, const int y) {
-                    const bool sw = key[y] < key[x];
-                    const float kx = key[x];
-                    const int32_t rx = ref[x];
-                    key[x] = sw ? key[y] : kx; key[y] = sw ? kx : key[y];
-                    ref[x] = sw ? ref[y] : rx; ref[y] = sw ? rx : ref[y];
-                };
-                cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
-                int32_t enter = kNone;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (key[j] != INFINITY && ~ref[j] >= kDirectCurve)
-                        out[nc++] = CurveCand{(uint32_t)(~ref[j] - kDirectCurve), __float_as_uint(key[j])};
-#pragma unroll
-                for (int j = 3; j >= 0; --j)
-                    if (key[j] != INFINITY && !(~ref[j] >= kDirectCurve)) {
-                        if (enter != kNone) push(enter);
-                        enter = ref[j];
-                    }
-                node = enter != kNone ? enter : pop();
-            }
-        } else if (~node >= kDirectCurve) {
-            out[nc++] = CurveCand{(uint32_t)(~node - kDirectCurve), 0u};
-            node = pop();
-        } else {
-            const BvhLeaf L = sc.bleaf[~node];
-            if (nc > 0u && nc + (uint32_t)L.bn > K) stop = true;
-            else {
-                if (L.sn + L.mn > 0) {                 // spheres in the curve tree: the ray again
-                    const RayRec R = st.ray[i];
-                    const v3 o = mk(R.ox, R.oy, R.oz), d = mk(R.dx, R.dy, R.dz);
-                    const double tm = depth0 ? st.tm[i] : 0.0;
-                    const double a = dot(d, d), ia = 1.0 / a;
-                    for (int q = L.sb; q < L.sb + L.sn; ++q) {
-                        const SphereRec S = sc.sph[q];
-                        sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + q, closest, best);
-                    }
-                    for (int q = L.mb; q < L.mb + L.mn; ++q) {
-                        const MSphereRec S = sc.msph[q];
-                        const double frac = (tm - S.t0) / S.den;
-                        const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                        sphere_test(o, d, a, ia, cen, S.rr, bm + q, closest, best);
-                    }
-                }
-                for (int b = L.bb; b < L.bb + L.bn && nc < K; ++b) out[nc++] = CurveCand{(uint32_t)b, 0u};
-                node = pop();
-            }
-        }
-        if (stop || node == kNone) {                  // the ray's list for this round is done
-            cw.closest[k] = closest;
-            cw.best[k] = best;
-            cw.ncand[k] = nc | (node != kNone ? 0x80000000u : 0u);
-            if (node != kNone) {
-                sv[0] = node;
-                sv[1] = sp;
-                for (int e = 0; e < min(sp, LDS); ++e) sv[2 + e] = (int32_t)lstk[e * 256];
-            }
-            if (g_split_dbg_on) {
-                atomicAdd(&g_split_dbg[0], (unsigned long long)nc);
-                atomicAdd(&g_split_dbg[2], (unsigned long long)dbg_nodes);
-                atomicAdd(&g_split_dbg[3], 1ull);
-            }
-            active = false;
-        }
     }
 }
 
@@ -3365,14 +3204,10 @@ static bool curve_debug() {                 // RTAMD_CURVE_DEBUG=1: the split ex
     const char* e = std::getenv("RTAMD_CURVE_DEBUG");
     return e != nullptr && e[0] == '1';
 }
-static bool trav_persist() {                // RTAMD_TRAV_PERSIST=1: k_curve_trav_p (persistent, refilling lanes)
-    const char* e = std::getenv("RTAMD_TRAV_PERSIST");
-    return e != nullptr && e[0] == '1';
-}
 #ifndef RT_CURVE_SPLIT_DEFAULT
 #define RT_CURVE_SPLIT_DEFAULT 0       // the split curve extend by default (RTAMD_CURVE_SPLIT=0 / 1 overrides)
 #endif
-static bool curve_split() {                 // RTAMD_CURVE_SPLIT=1 / 0: the split / one-kernel curve extend
+bool curve_split() {                        // RTAMD_CURVE_SPLIT=1 / 0: the split / one-kernel curve extend
     const char* e = std::getenv("RTAMD_CURVE_SPLIT");   // read per launch: tests switch it inside one process
     return e != nullptr && e[0] != '\0' ? e[0] != '0' : RT_CURVE_SPLIT_DEFAULT != 0;
 }
@@ -3405,14 +3240,6 @@ static hipError_t launch_curves_split(const DevScene& sc, const RenderParams& rp
                                       unsigned int* claim, const CurveSplit& cs, hipStream_t s) {
     uint32_t occ = 0;
     HIP_RETURN_IF(curve_occupancy(reinterpret_cast<const void*>(&k_extend_curves<true>), 0, &occ));
-    uint32_t tocc = 0;                                            // k_curve_trav_p's resident blocks
-    if (trav_persist()) {
-        int per_cu = 0, cus = 0, dev = 0;
-        HIP_RETURN_IF(hipGetDevice(&dev));
-        HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_curve_trav_p<false>, 256, 0));
-        HIP_RETURN_IF(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        tocc = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
-    }
     const int dbg = curve_debug() ? 1 : 0;
     HIP_RETURN_IF(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_split_dbg_on), &dbg, sizeof dbg, 0, hipMemcpyHostToDevice, s));
     if (occ > curve_blocks()) occ = curve_blocks();
@@ -3430,16 +3257,7 @@ static hipError_t launch_curves_split(const DevScene& sc, const RenderParams& rp
             HIP_RETURN_IF(hipMemsetAsync(cs.cnt[cur], 0, sizeof(uint32_t), s));
             HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
             const uint32_t tb = (m + 255u) / 256u;
-            if (trav_persist()) {                                 // resident blocks refill from the list
-                uint32_t pt = tb < tocc ? tb : tocc;
-                if (pt == 0u) pt = 1u;
-                if (round == 0)
-                    hipLaunchKernelGGL(k_curve_trav_p<false>, dim3(pt), dim3(256), 0, s, sc, st, in, k0, m, w, depth0, claim);
-                else
-                    hipLaunchKernelGGL(k_curve_trav_p<true>, dim3(pt), dim3(256), 0, s, sc, st, in, k0, m, w, depth0, claim);
-                HIP_RETURN_IF(hipGetLastError());
-                HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-            } else if (round == 0)
+            if (round == 0)
                 hipLaunchKernelGGL(k_curve_trav<false>, dim3(tb), dim3(256), 0, s, sc, st, in, k0, m, w, depth0);
             else
                 hipLaunchKernelGGL(k_curve_trav<true>, dim3(tb), dim3(256), 0, s, sc, st, in, k0, m, w, depth0);

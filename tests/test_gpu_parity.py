@@ -510,10 +510,8 @@ def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     # extend (also with 3 blocks)
     for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {"RTAMD_CURVE_SPLIT": "1"},
                 {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_BLOCKS": "3"}, {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_K": "5"},
-                {"RTAMD_CURVE_SPLIT": "1", "RTAMD_TRAV_PERSIST": "1", "RTAMD_CURVE_K": "5"},
-                {"RTAMD_CURVE_SPLIT": "1", "RTAMD_TRAV_PERSIST": "1"},
                 {"RTAMD_CURVE_SPLIT": "0"}, {"RTAMD_CURVE_BLOCKS": "3"}):
-        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_K", "RTAMD_CURVE_SPLIT", "RTAMD_TRAV_PERSIST"):
+        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_K", "RTAMD_CURVE_SPLIT"):
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)
