@@ -48,6 +48,23 @@ def test_library_loads_and_reports_errors_without_gpu():
         _lib.call("rt_shard_pixels", 4, 4, 5, 2, None, ctypes.byref(ctypes.c_int64()))
 
 
+def test_new_abi_entry_points_refuse_bad_handles_without_gpu():
+    """ABI 6 entry points check their handles and arguments before any device or RCCL call."""
+    L = _lib.lib()
+    h = ctypes.c_int(0)
+    uid = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES)()
+    assert L.rt_comm_create(424242, uid, 0, 1, ctypes.byref(h)) != 0
+    assert b"invalid context" in L.rt_last_error()
+    assert L.rt_comm_create(424242, uid, 2, 2, ctypes.byref(h)) != 0
+    assert b"rank" in L.rt_last_error()
+    assert L.rt_gather_shards(424242, 4, 4, None, None, None) != 0
+    assert b"invalid communicator" in L.rt_last_error()
+    assert L.rt_comm_destroy(424242) != 0
+    assert L.rt_curve_depth_probe(424242, 1, None, None, None) != 0
+    assert b"invalid context" in L.rt_last_error()
+    assert L.rt_context_set_option(424242, _lib.RT_OPTIONS["exact_libm"], 1) != 0
+
+
 def test_random_scene_structure():
     sc = scenes.random_scene(200, 100)
     objs = sc.obj_list
