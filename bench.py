@@ -31,7 +31,7 @@ lane, HIP events on the lane's stream; with two lanes in the timed region it
 comes from one extra untimed single-lane frame, and the overlapped figure is
 `roofline_two_lane`); `roofline_frame` is the whole path's algorithmic bytes
 per frame over ms_per_step.  PMC-derived `traffic` / `valu` / `valu_issue`
-come from profiles/pmc_*.json only when those carry this rt_kernels.hip's hash.
+come from profiles/pmc/<scene>_*.json only when those carry this rt_kernels.hip's hash.
 """
 import argparse
 import json
@@ -395,16 +395,15 @@ def pmc_path(kind, scene):
 
 
 def load_pmc(kind, scene):
-    """The scene's PMC summary (profiles/pmc/<scene>_<kind>.json; profiles/pmc_<kind>.json, the C2 summary
-    of earlier rounds, as a fallback) if it was measured on this scene with these kernels, else None.
-    Returns (summary, path relative to the repo)."""
-    for path in (pmc_path(kind, scene), os.path.join(ROOT, "profiles", "pmc_%s.json" % kind)):
-        if not os.path.exists(path):
-            continue
-        with open(path) as f:
-            pm = json.load(f)
-        if pm.get("scene") == scene and pm.get("kernel_sha16") == kernel_sha16():
-            return pm, os.path.relpath(path, ROOT)
+    """The scene's PMC summary (profiles/pmc/<scene>_<kind>.json) if it was measured on this scene with
+    these kernels, else None.  Returns (summary, path relative to the repo)."""
+    path = pmc_path(kind, scene)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pm = json.load(f)
+    if pm.get("scene") == scene and pm.get("kernel_sha16") == kernel_sha16():
+        return pm, os.path.relpath(path, ROOT)
     return None, None
 
 

@@ -16,6 +16,6 @@ for s in c2 c5; do
   grep '^{' $O/bench_$s.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline'] or {}; f=d.get('roofline_frame') or {}; p=d.get('parity') or {}; q=d.get('parity_frame') or {}; print('$s', d['value'], d['ms_per_step'], 'roof', r.get('frac'), 'frame', f.get('frac'), 'parity', p.get('rms_vs_oracle'), p.get('pixels_gt_1e-9'), 'frame_rows', q.get('rms_vs_oracle'), q.get('pixels_gt_1e-9'), 'cpu', (d.get('cpu_baseline') or {}).get('value'))"
 done
 timeout -k 10 600 bash tools/profile_round.sh ${TAG}_c2 > $O/prof_c2.log 2>&1 || { echo "profile C2 failed"; tail -5 $O/prof_c2.log; exit 1; }
-mkdir -p $O/pmc_c2 && cp profiles/pmc_round.json profiles/pmc_extend.json profiles/pmc_shade.json $O/pmc_c2/
+mkdir -p $O/pmc_c2 && cp profiles/pmc/*.json $O/pmc_c2/
 timeout -k 10 600 bash tools/profile_round.sh ${TAG}_c5 --scene curves --spp 4 > $O/prof_c5.log 2>&1 || { echo "profile C5 failed"; tail -5 $O/prof_c5.log; exit 1; }
 echo done

@@ -18,9 +18,8 @@ cycles waiting (SQ_WAIT_ANY / wave cycles), occupancy, and per item VALU /
 SALU / LDS instructions and f64 lane-ops.  Derived percentages are averaged
 over dispatches weighted by GRBM_GUI_ACTIVE (each dispatch's busy cycles).
 
-It also writes profiles/pmc/<scene>_extend.json and <scene>_shade.json (and,
-for the cover scene, profiles/pmc_extend.json / pmc_shade.json), which bench.py
-reads for roofline.traffic and the valu / valu_issue objects.
+It also writes profiles/pmc/<scene>_extend.json and <scene>_shade.json, which
+bench.py reads for roofline.traffic and the valu / valu_issue objects.
 """
 import collections
 import csv
@@ -165,14 +164,10 @@ def main():
     for rec in (report, pmc_ext, pmc_sh):
         rec["kernel_sha16"] = sha
     json.dump(report, open(out_path, "w"), indent=1)
-    # per scene (bench.py load_pmc: profiles/pmc/<scene>_{extend,shade}.json); the C2 summaries also
-    # under their earlier names
+    # per scene (bench.py load_pmc: profiles/pmc/<scene>_{extend,shade}.json)
     os.makedirs(os.path.join(ROOT, "profiles", "pmc"), exist_ok=True)
     json.dump(pmc_ext, open(os.path.join(ROOT, "profiles", "pmc", "%s_extend.json" % report["scene"]), "w"), indent=1)
     json.dump(pmc_sh, open(os.path.join(ROOT, "profiles", "pmc", "%s_shade.json" % report["scene"]), "w"), indent=1)
-    if report["scene"] == "cover":
-        json.dump(pmc_ext, open(os.path.join(ROOT, "profiles", "pmc_extend.json"), "w"), indent=1)
-        json.dump(pmc_sh, open(os.path.join(ROOT, "profiles", "pmc_shade.json"), "w"), indent=1)
     print(json.dumps(report, indent=1))
 
 

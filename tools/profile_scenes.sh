@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-5 PMC profile sets for every benchmark scene (tools/profile_round.sh per scene), so each bench line
+# carries traffic / valu / valu_issue from profiles/pmc/<scene>_{extend,shade}.json (kernel-hash stamped).
+#   usage: tools/profile_scenes.sh TAG
+set -o pipefail
+TAG=${1:-r05}
+run() { name=$1; shift; timeout -k 10 900 bash tools/profile_round.sh ${TAG}_$name "$@" > gpurun_out/prof_${TAG}_$name.log 2>&1 || { echo "profile $name failed"; tail -5 gpurun_out/prof_${TAG}_$name.log; exit 1; }; echo "profile $name ok"; }
+mkdir -p gpurun_out
+run c2
+run c5 --scene curves --spp 4
+run c3 --scene cover_marble --spp 256
+run c4 --scene cornell --nx 1024 --ny 1024 --spp 256
+run c4m --scene cornell_mixture --nx 1024 --ny 1024 --spp 256
+ls profiles/pmc/
