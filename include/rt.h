@@ -272,7 +272,7 @@ typedef struct rt_stats {
     double   ms_extend;   /* summed device time of the extend (closest-hit) kernel */
     double   ms_shade;    /* summed device time of the shade kernel */
     uint64_t extend_launches;
-    uint64_t extend_rays; /* = segments */
+    uint64_t extend_rays; /* segments the extend kernels traced (the wavefront launches and the fused curve extend; the rest ran in the tail kernel) */
     uint32_t max_depth_seen;  /* deepest wavefront iteration (the tail runs in k_finish) */
     uint32_t reserved;
     double   ms_finish;       /* summed device time of the tail kernel */

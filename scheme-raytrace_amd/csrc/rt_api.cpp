@@ -23,7 +23,8 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, const CurveSplit*, hipStream_t);
+                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, const CurveSplit*, const CurveFuse*,
+                         hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t, hipStream_t);
 hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
@@ -40,6 +41,7 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t launch_scatter_pixels(const double*, const uint32_t*, uint32_t, double*, hipStream_t);
 bool curve_split();
+bool curve_persistent();
 hipError_t launch_curve_depth(const double*, const double*, uint32_t, int32_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
 hipError_t take_curve_stats(unsigned long long out[2]);
@@ -1273,10 +1275,28 @@ hipError_t ensure_curve_split(Lane& L, const DevScene& d, const size_t pool) {
 // Scenes whose world BVH holds curves run the persistent curve kernel, whose
 // grid fills the chip by itself: a second lane's kernels only queue behind it
 // and its narrow tails, so one lane is faster (C5 at 64 spp: 200.3 vs 164.1
-// Mrays/s, profiles/r03/ab/ab_lanes_c5.log).  RT_OPT_LANES overrides.
+// Mrays/s, profiles/r03/ab/ab_lanes_c5.log; round 5, 398.0 vs 304.9 at 32 spp and
+// 409.1 vs 306.5 at 256 spp, profiles/r05/ab/lanes/).  RT_OPT_LANES overrides.
 int lanes_for(const Context& c, const DevScene& d) {
     if (c.opt_lanes > 0) return lanes_wanted(c);
     return curve_kernel_scene(d) ? 1 : lanes_wanted(c);
+}
+
+// The fused curve extend (rt_kernels.hip k_extend_curves<FUSE>: every depth >= 1 of a chunk in one launch)
+// serves curve-kernel scenes whose hits it can shade itself: no Perlin tables (the fused kernel keeps no
+// LDS copy of them) and no light mixture (f2).  It pays where the per-depth launches are small: each
+// persistent launch drains once (~1.1 ms at C5), which a depth-1 launch of n rays amortises over n.  C5,
+// fused vs one launch per depth (profiles/r05/ab/fuse/): 1 spp 275.2 vs 189.5 Mrays/s, 8 spp 380.4 vs
+// 356.1, 32 spp 394.8 vs 395.8, 256 spp (128-spp chunks) 402.9 vs 407.8 — so it is taken for depth-1
+// launches of at most kFuseMaxRays rays (full frames below ~16 spp per chunk, e.g. the progressive
+// one-pass-at-a-time loop, main.scm:533-544).  RTAMD_CURVE_FUSE=0 / 1: never / always (A/B, tests).
+constexpr uint32_t kFuseMaxRays = 1u << 24;
+bool curve_fuse(const DevScene& d, const uint32_t n) {
+    if (!(curve_kernel_scene(d) && curve_persistent() && !d.has_perlin && d.light.type == LIGHT_OFF)) return false;
+    const char* e = std::getenv("RTAMD_CURVE_FUSE");   // read per render: tests switch it inside one process
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return n <= kFuseMaxRays;
 }
 
 // A chunk's live paths at or below max(tail_threshold, B / tail_divisor) go to
@@ -1407,12 +1427,13 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         HIPCHK(L.hit.ensure(4 * scap * sizeof(HitRec)));   // the 4 material hit queues (sharded like the survivors)
         HIPCHK(L.sb.ensure(cap * 3 * sizeof(double)));
         HIPCHK(L.counts.ensure(kIters * kCountsPerIter * sizeof(uint32_t)));
-        HIPCHK(L.seg_tail.ensure(3 * sizeof(unsigned long long)));   // tail segments, next tail path, errors
+        // tail segments, next tail path / curve claim, LDS errors, the fused curve extend's continuation segments
+        HIPCHK(L.seg_tail.ensure(4 * sizeof(unsigned long long)));
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
         if (curve_kernel_scene(s->dev) && curve_split()) HIPCHK(ensure_curve_split(L, s->dev, cap));
         else if (L.cs.cap) { L.cs = CurveSplit{}; L.cw_buf.release(); }   // (the previous render drained the lane)
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
-        HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 3 * sizeof(unsigned long long), L.stream));
+        HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 4 * sizeof(unsigned long long), L.stream));
         L.A = carve_state(L.st_a.p, scap);
         L.B = carve_state(L.st_b.p, scap);
         L.state = Lane::IDLE;
@@ -1463,6 +1484,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             return 0;
         }
         uint32_t* cnt = L.counts.as<uint32_t>() + L.depth * kCountsPerIter;   // [material][shard], survivors at 4
+        bool fused = false;
         HitBuf hit{L.hit.as<HitRec>(), (uint32_t)scap};
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[0], L.stream));
         if (L.depth == 0 && L.fused_camera)     // raygen + first closest hit in one kernel
@@ -1476,14 +1498,17 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             DevScene dl = s->dev;
             if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lds4);
             if (dl.bez_ring) dl.bez_ring += (size_t)L.index * dl.ring_waves * kBezRing * 16u;
+            // the fused curve extend (k_extend_curves<FUSE>): every depth from 1 on in this one launch
+            CurveFuse fz{L.seg_tail.as<unsigned long long>() + 3, (uint32_t)L.depth};
+            fused = L.depth > 0 && curve_fuse(s->dev, L.n) && !(L.cs.cap && curve_split());
             HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
                                  reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1),
-                                 L.cs.cap ? &L.cs : nullptr, L.stream));
+                                 L.cs.cap ? &L.cs : nullptr, fused ? &fz : nullptr, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
-        for (int mt = 0; mt < 4; ++mt) {
+        for (int mt = 0; mt < 4 && !fused; ++mt) {         // (a fused launch shades its hits itself: no queues)
             if (!(s->dev.mat_mask & (1 << mt))) continue;
             const QView qv{cnt + mt * kShards * kCntStride, (uint32_t)shard_cap};
             HIPCHK(launch_shade(mt, s->dev, s->d_dev.as<const DevScene>(), L.rp, *L.cur, hit, qv, L.n, *L.nxt, surv,
@@ -1525,6 +1550,9 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         L.view = QView{L.counts.as<uint32_t>() + L.depth * kCountsPerIter + 4 * kShards * kCntStride,
                        (uint32_t)shard_cap};
         std::swap(L.cur, L.nxt);
+        static const bool dbg_depth = std::getenv("RTAMD_DEBUG_DEPTH") != nullptr;   // diagnostics: live paths per depth
+        if (dbg_depth) std::fprintf(stderr, "depth-count lane %d chunk %d depth %d in %u out %u\n", L.index, L.chunk,
+                                    L.depth, L.n, n);
         L.n = n;
         ++L.depth;
         return step(L);
@@ -1609,11 +1637,12 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     }
     for (int li = 0; li < nlanes; ++li) {
         Lane& L = *c->lanes[li];
-        unsigned long long ctl[3] = {0, 0, 0};
+        unsigned long long ctl[4] = {0, 0, 0, 0};
         HIPCHK(hipMemcpy(ctl, L.seg_tail.p, sizeof ctl, hipMemcpyDeviceToHost));
         if (ctl[2]) return fail("internal: a persistent kernel's LDS allocation was too small (flags " +
                                 std::to_string(ctl[2]) + ")");
-        s->stats.segments += ctl[0];
+        s->stats.segments += ctl[0] + ctl[3];
+        s->stats.extend_rays += ctl[3];                // the fused curve extend's segments past its launch's rays
         for (size_t k = 0; k < L.n_fin; ++k) {
             float a = 0;
             HIPCHK(hipEventElapsedTime(&a, L.ev_fin[k].first, L.ev_fin[k].second));

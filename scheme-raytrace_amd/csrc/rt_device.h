@@ -263,6 +263,15 @@ struct CurveWork {
     uint32_t* cont_n;         // ... and their count
     uint32_t K, S;
     int32_t lds;              // k_curve_trav's stack entries per lane in LDS (<= RT_TRAV_LDS_STACK; tests lower it)
+    unsigned long long* segs; // the fused curve extend (FUSE): continuation segments counter
+    uint32_t depth;           // ... and the launch's path depth
+    uint32_t fin_batch;       // ... and its finish batch (finished lanes shaded and refilled together)
+};
+
+// Host side: the fused curve extend's launch (launch_extend): every depth from `depth` on in one launch
+struct CurveFuse {
+    unsigned long long* segs;
+    uint32_t depth;
 };
 
 // Host side: a render lane's split-curve buffers (rt_api.cpp Lane::cs), handed to launch_extend.

@@ -1927,7 +1927,16 @@ static_assert(4 * sizeof(CurveWave<true>) <= 160 * 1024 / RT_CURVE_LIST_WAVES,
 // visited by k_curve_trav, [3] rays listed (summed over rounds)
 __device__ unsigned long long g_split_dbg[4];
 __device__ int g_split_dbg_on;
-template <bool LIST>
+// FUSE (1: device libm, 2: the exact libm; !LIST): every depth from cw.depth on in one launch.  A lane
+// whose ray is resolved shades it on the spot (shade_hit, the wavefront shade's own code: any material,
+// no Perlin tables, no light mixture — launch_extend checks the scene) and, if the path goes on, stores
+// the scattered ray in place (same slot) and walks it at once, so the launch drains once per chunk
+// instead of once per depth (C5: ~1.1 ms per depth launch, about a quarter of the curve kernel's time).
+// Paths that end write their sample; continuation segments are counted into *cw.segs.
+template <bool EX>
+__device__ __forceinline__ bool fused_shade(const DevScene& sc, const RenderParams& rp, PathRegs& p, const double t,
+                                            const int32_t leaf, v3& L);   // below shade_hit
+template <bool LIST, int FUSE = 0>
 __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
@@ -1943,8 +1952,10 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     int gb = 0;                                     // the world BVH group (commit_scene builds at most one)
     while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
+    static_assert(!(LIST && FUSE), "the fused curve extend walks the tree");
     bool active = false, exhausted = false, trav = false;
     uint32_t i = 0, queued = 0;
+    uint32_t dep = FUSE ? cw.depth : 0u, fsegs = 0;  // FUSE: the lane's path depth, continuation segments
     // LIST: the lane's ray (slice-local), its list cursor and length, whether its traversal goes on in the
     // next round, and the next candidate (loaded one iteration ahead)
     uint32_t k = 0, cj = 0, nc = 0;
@@ -1982,6 +1993,23 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
     auto pop = [&]() -> int32_t {
         --sp;
         return (int32_t)(sp < lds4 ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lds4) * sc.ovf_lanes + ovf_lane]);
+    };
+    // a lane takes ray i (its closest hit from scratch): the groups before the BVH, then the BVH4 walk (!LIST)
+    auto start_ray = [&]() {
+        v3 o, d;
+        double tm;
+        ray_of(o, d, tm);
+        closest = kTmax;
+        best = -1;
+        for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
+        bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
+        br = box_ray_w(o, d);
+        tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
+        bez_ray(o, d, W.ray[lane]);
+        sp = 0; node = sc.bvh4_root; trav = gb < sc.n_groups;
+#if RT_CURVE_PREFETCH
+        if (trav && node >= 0) N = sc.bvh4[node];
+#endif
     };
     uint32_t qn = 0, svn = 0;                       // wave-uniform: queued candidates, survivors
     // the wave's survivor ring (launch_extend_curves keeps the grid within sc.ring_waves) and the ring
@@ -2026,10 +2054,34 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         // round trips, which cost the wave the same whether one lane or sixteen take them.
         const bool fin = active && !trav && pb >= pe && W.done[lane] == queued;
         const unsigned long long fin_m = __ballot(fin);
-        const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= RT_CURVE_FINISH_BATCH ||
+        const int fin_batch = FUSE ? (int)cw.fin_batch : RT_CURVE_FINISH_BATCH;   // FUSE: the batch shades too
+        const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= fin_batch ||
                                              fin_m == __ballot(active));
         bool cont = false;                                   // LIST: handed back to the next round
-        if (fin && flush && LIST && tmore) {
+        if constexpr (FUSE != 0) {
+            if (fin && flush) {                              // shade here; a scattered path goes on in this lane
+                PathRegs p;
+                load_path(st, i, p, rp, dep);
+                for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<0>(sc, sc.groups[g], p.o, p.d, p.time, closest, best, nullptr);
+                v3 L;
+                bool go = false;
+                if (best < 0) L = sky_radiance(sc, p.d);
+                else go = fused_shade<FUSE == 2>(sc, rp, p, closest, best, L);
+                if (go) {
+                    store_path(st, i, p);
+                    dep = p.depth;
+                    ++fsegs;
+                    start_ray();
+                    W.done[lane] = 0u;
+                    queued = 0u;
+                    pb = pe = 0;
+                    ray_it = 0;
+                } else {
+                    write_sample(rp, p, L);
+                    active = false;
+                }
+            }
+        } else if (fin && flush && LIST && tmore) {
             cw.closest[k] = closest;
             cw.best[k] = best;
             cont = true;
@@ -2061,9 +2113,11 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         // shard, k / 256, spread a batch over several shards, one dependent atomic each: -0.8 % at C5).
         // Waves claim rays dynamically, so a shard's share is not bounded by n / kShards: a full shard
         // spills into the next (wave_append<true>)
-        const uint32_t slot = wave_append<true>(cls, (blockIdx.x * 4u + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1),
-                                                counts, shard_cap);
-        if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
+        if constexpr (FUSE == 0) {
+            const uint32_t slot = wave_append<true>(cls, (blockIdx.x * 4u + (threadIdx.x >> 6)) & (uint32_t)(kShards - 1),
+                                                    counts, shard_cap);
+            if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
+        }
         if constexpr (LIST) {                                // the continuation list: one atomic per wave
             const unsigned long long cm = __ballot(cont);
             if (cm) {
@@ -2108,20 +2162,8 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
                         if (trav) nxt = reinterpret_cast<const uint2*>(cw.cand)[(size_t)k * cw.K];
                     } else {
                         i = qphys(qm, kk);
-                        v3 o, d;
-                        double tm;
-                        ray_of(o, d, tm);
-                        closest = kTmax;
-                        best = -1;
-                        for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
-                        bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
-                        br = box_ray_w(o, d);
-                        tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
-                        bez_ray(o, d, W.ray[lane]);
-                        sp = 0; node = sc.bvh4_root; trav = gb < sc.n_groups;
-#if RT_CURVE_PREFETCH
-                        if (trav && node >= 0) N = sc.bvh4[node];
-#endif
+                        dep = FUSE ? cw.depth : 0u;
+                        start_ray();
                     }
                     W.done[lane] = 0u;
                     queued = 0u;
@@ -2283,6 +2325,10 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
                 wave_sync();
             }
         }
+    }
+    if constexpr (FUSE != 0) {                       // continuation segments: wave sum, one atomic per wave
+        for (int off = 32; off > 0; off >>= 1) fsegs += __shfl_xor(fsegs, off, 64);
+        if (lane == 0u && fsegs) atomicAdd(cw.segs, (unsigned long long)fsegs);
     }
 #ifdef RT_STATS
     RT_STAT(20, st_steps); RT_STAT(21, st_busy); RT_STAT(22, st_wait);
@@ -2986,6 +3032,14 @@ __device__ __forceinline__ bool shade_hit(const DevScene& sc, const PerlinLds& P
     return true;
 }
 
+// the fused curve extend's shading (k_extend_curves<FUSE>): any material, no Perlin tables (PN false: the
+// table reference is never read), no light mixture
+template <bool EX>
+__device__ __forceinline__ bool fused_shade(const DevScene& sc, const RenderParams& rp, PathRegs& p, const double t,
+                                            const int32_t leaf, v3& L) {
+    return shade_hit<-1, false, false, EX>(sc, *reinterpret_cast<const PerlinLds*>(sc.leaves), rp, p, t, leaf, L, sc.leaves);
+}
+
 template <bool PN = true>
 __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
     if (PN && sc.has_perlin) {   // the Perlin tables (perlin.scm:32-36 data) into LDS
@@ -3200,6 +3254,7 @@ static uint32_t curve_blocks() {            // cap on the persistent curve grid 
     const char* e = std::getenv("RTAMD_CURVE_BLOCKS");  // read per launch: tests switch it inside one process
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
 }
+bool curve_persistent() { return curve_blocks() > 0u; }   // the host's check before a fused launch
 static bool curve_debug() {                 // RTAMD_CURVE_DEBUG=1: the split extend's rounds on stderr (diagnostics)
     const char* e = std::getenv("RTAMD_CURVE_DEBUG");
     return e != nullptr && e[0] == '1';
@@ -3213,13 +3268,15 @@ bool curve_split() {                        // RTAMD_CURVE_SPLIT=1 / 0: the spli
 }
 // resident blocks of a curve kernel instance for its dynamic LDS, cached per (kernel, device, LDS bytes)
 static hipError_t curve_occupancy(const void* f, const size_t lds, uint32_t* out) {
-    static const void* occ_f[2] = {nullptr, nullptr};
-    static int occ_dev[2] = {-1, -1};
-    static size_t occ_lds[2] = {~(size_t)0, ~(size_t)0};
-    static uint32_t occ_blocks[2] = {0, 0};
+    static const void* occ_f[4] = {nullptr, nullptr, nullptr, nullptr};
+    static int occ_dev[4] = {-1, -1, -1, -1};
+    static size_t occ_lds[4] = {~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0};
+    static uint32_t occ_blocks[4] = {0, 0, 0, 0};
     int dev = 0;
     HIP_RETURN_IF(hipGetDevice(&dev));
-    const int slot = f == reinterpret_cast<const void*>(&k_extend_curves<true>) ? 1 : 0;
+    const int slot = f == reinterpret_cast<const void*>(&k_extend_curves<true>) ? 1
+                   : f == reinterpret_cast<const void*>(&k_extend_curves<false, 1>) ? 2
+                   : f == reinterpret_cast<const void*>(&k_extend_curves<false, 2>) ? 3 : 0;
     if (occ_f[slot] != f || occ_lds[slot] != lds || occ_dev[slot] != dev) {
         int per_cu = 0, cus = 0;
         HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, lds));
@@ -3289,7 +3346,8 @@ static hipError_t launch_curves_split(const DevScene& sc, const RenderParams& rp
 }
 hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t shard_cap,
-                         uint32_t* counts, bool depth0, unsigned int* claim, const CurveSplit* cs, hipStream_t s) {
+                         uint32_t* counts, bool depth0, unsigned int* claim, const CurveSplit* cs,
+                         const CurveFuse* fuse, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
     // the persistent curve kernel: every curve in the world BVH (its groups outside the BVH are spheres and
@@ -3301,7 +3359,10 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
         // holds lds4 entries per lane (the rest in the overflow area).  Occupancy per (device, LDS bytes)
         const size_t clds = (size_t)256 * (size_t)(sc.lds4 > 0 ? sc.lds4 : 1) * sizeof(uint32_t);
         uint32_t occ_blocks = 0;
-        HIP_RETURN_IF(curve_occupancy(reinterpret_cast<const void*>(&k_extend_curves<false>), clds, &occ_blocks));
+        const void* kf = !fuse ? reinterpret_cast<const void*>(&k_extend_curves<false, 0>)
+                       : rp.exact_libm ? reinterpret_cast<const void*>(&k_extend_curves<false, 2>)
+                                       : reinterpret_cast<const void*>(&k_extend_curves<false, 1>);
+        HIP_RETURN_IF(curve_occupancy(kf, clds, &occ_blocks));
         uint32_t pb = blocks < occ_blocks ? blocks : occ_blocks;
         if (pb > curve_blocks()) pb = curve_blocks();
         // the overflow area holds sc.ovf_lanes lanes per render lane: never launch more (ovf_lane indexes it)
@@ -3309,10 +3370,27 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
         if (pb > sc.ring_waves / 4u) pb = sc.ring_waves / 4u;   // one survivor ring per wave
         if (pb == 0u) pb = 1u;
         HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-        hipLaunchKernelGGL(k_extend_curves<false>, dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
-                           shard_cap, counts, depth0, claim, CurveWork{}, 0u);
+        CurveWork w{};
+        if (!fuse) {
+            hipLaunchKernelGGL((k_extend_curves<false, 0>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                               shard_cap, counts, depth0, claim, w, 0u);
+        } else {
+            w.segs = fuse->segs;
+            w.depth = fuse->depth;
+            {
+                static const int fb = std::getenv("RTAMD_FUSE_BATCH") ? std::atoi(std::getenv("RTAMD_FUSE_BATCH")) : 0;
+                w.fin_batch = fb > 0 ? (uint32_t)fb : (uint32_t)RT_CURVE_FINISH_BATCH;
+            }
+            if (rp.exact_libm)
+                hipLaunchKernelGGL((k_extend_curves<false, 2>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                                   shard_cap, counts, false, claim, w, 0u);
+            else
+                hipLaunchKernelGGL((k_extend_curves<false, 1>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                                   shard_cap, counts, false, claim, w, 0u);
+        }
         return hipGetLastError();
     }
+    if (fuse) return hipErrorNotSupported;           // only the persistent curve kernel shades its own hits
 #define RT_EXTEND_F(F)                                                                                      \
     hipLaunchKernelGGL((k_extend<F>), dim3(blocks), dim3(256), lds, s, sc, rp, st, in, n, hit,             \
                        shard_cap, counts, depth0)

@@ -507,11 +507,13 @@ def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     imgs = []
     # the flat list, the per-ray kernel, the split curve extend (k_curve_trav + k_extend_curves<true>; with
     # 3 blocks; with 5-candidate lists, so rays continue over many rounds), the one-kernel persistent curve
-    # extend (also with 3 blocks)
+    # extend fused over the depths (the default: hits shaded in the kernel, every material of the scene;
+    # also with 3 blocks), and one launch per depth (RTAMD_CURVE_FUSE=0, also with 3 blocks)
     for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {"RTAMD_CURVE_SPLIT": "1"},
                 {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_BLOCKS": "3"}, {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_K": "5"},
-                {"RTAMD_CURVE_SPLIT": "0"}, {"RTAMD_CURVE_BLOCKS": "3"}):
-        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_K", "RTAMD_CURVE_SPLIT"):
+                {"RTAMD_CURVE_SPLIT": "0"}, {"RTAMD_CURVE_BLOCKS": "3"}, {"RTAMD_CURVE_FUSE": "0"},
+                {"RTAMD_CURVE_FUSE": "0", "RTAMD_CURVE_BLOCKS": "3"}):
+        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_K", "RTAMD_CURVE_SPLIT", "RTAMD_CURVE_FUSE"):
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)
