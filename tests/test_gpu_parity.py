@@ -460,6 +460,54 @@ def test_wavefront_matches_tail_kernel_bitwise(sched, monkeypatch, name):
     assert np.array_equal(a, b), np.abs(a - b).max()
 
 
+@pytest.mark.parametrize("libm", ["exact", "device"])
+def test_fused_curve_extend_bitwise(sched, monkeypatch, libm):
+    """The fused curve extend (k_extend_curves<FUSE>: every depth >= 1 in one launch, hits shaded in the
+    kernel) in both libm instances (FUSE 2: the exact sin / cos; FUSE 1: the device's) against one launch
+    per depth with the wavefront shade kernels, on a scene with every material (lambertian curves and
+    walls, metal, glass, a light, moving spheres) at a production-sized launch (2 lanes, 4 chunks): the
+    same image bit for bit, and the same segment count."""
+    from rtamd import scene as g, vec as v
+    from rtamd.rng import HostStream
+    nx, ny, spp = 320, 240, 8
+    rr = HostStream(0x5EED0105)
+    red = g.make_lambertian(g.constant_texture(v.vec3(0.65, 0.05, 0.05)))
+    white = g.make_lambertian(g.constant_texture(v.vec3(0.73, 0.73, 0.73)))
+    metal = g.make_metal(g.constant_texture(v.vec3(0.8, 0.8, 0.7)), 0.1)
+    glass = g.make_dielectric(1.5)
+    light = g.make_diffuse_light(g.constant_texture(v.vec3(4, 4, 4)))
+    objs = [g.flip_normals(g.make_yz_rect(0, 555, 0, 555, 555, white)), g.make_xz_rect(0, 555, 0, 555, 0, white),
+            g.bezier_array(scenes.random_polyline_curves(2000), 3.0, red)]
+    for i in range(30):
+        c = v.vec3(60 + rr() * 430, 40 + rr() * 400, 60 + rr() * 430)
+        m = (white, metal, glass)[i % 3]
+        if i % 4 == 0:
+            objs.append(g.make_moving_sphere(c, v.vec3(c[0], c[1] + 20, c[2]), 0.0, 1.0, 15 + 10 * rr(), m))
+        else:
+            objs.append(g.make_sphere(c, 10 + 15 * rr(), m))
+    objs += [g.flip_normals(g.make_xz_rect(213, 343, 227, 332, 554, light)), g.make_yz_rect(0, 555, 0, 555, 0, red)]
+    sc = g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
+    sched.set_option("exact_libm", libm)
+    sched.set_option("lanes", 2)
+    sched.set_option("max_paths", nx * ny * 2)           # 4 chunks of 2 spp, each far above the tail threshold
+    imgs, segs = [], []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("RTAMD_CURVE_FUSE", fuse)
+        a = np.zeros(nx * ny * 3)
+        h = gpu.render_host(sc, nx, ny, 0, spp, SEED, a)
+        st = gpu.stats(h)
+        imgs.append(a)
+        segs.append(st.segments)
+        if fuse == "1":
+            assert st.shade_hits == 0 and st.finish_paths == 0     # depths >= 1 ran fused, no tail kernel
+        else:
+            assert st.shade_hits > 0
+    print("fused curve extend (%s libm): segments %d / %d" % (libm, segs[0], segs[1]))
+    assert np.isfinite(imgs[0]).all() and imgs[0].any()
+    assert np.array_equal(imgs[0], imgs[1]), np.abs(imgs[0] - imgs[1]).max()
+    assert segs[0] == segs[1]
+
+
 @pytest.mark.parametrize("flat_curves", [False, True])
 def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     """Curves, spheres and moving spheres in one world BVH between rect
