@@ -1301,8 +1301,19 @@ bool curve_fuse(const DevScene& d, const uint32_t n) {
 
 // A chunk's live paths at or below max(tail_threshold, B / tail_divisor) go to
 // the tail kernel; RT_OPT_TAIL_OFF keeps every depth in the wavefront.
-uint32_t tail_paths(const Context& c, const uint32_t B) {
+// Without those options the threshold also follows the render's shape (round 5, C2's scene, same images;
+// profiles/r05/ab/tail/): a render of one chunk has no second lane to fill its narrow depths, so the tail
+// kernel takes over at B/4 (1 spp per frame, the progressive loop: 2.60 → 2.13 ms); renders of a few
+// small chunks take it at up to B/64, at most 262 144 paths (4 spp: 4.85 → 4.17 ms; 16 spp: 12.7 → 11.3 ms);
+// large chunks keep B/256 (the 8-GPU per-rank share, 680×381×1024 spp: 73.6 ms at B/256, 75.1 at B/64; C2:
+// B/256 over B/128, rounds 2–3).  Curve-kernel scenes keep the fixed rule (their tail kernel walks curves
+// per ray; the fused curve extend serves their small launches).
+uint32_t tail_paths(const Context& c, const uint32_t B, const int nchunks, const bool curves) {
     if (c.wavefront_only) return 0u;
+    if (c.opt_tail_paths <= 0 && c.opt_tail_div <= 0 && !curves) {
+        if (nchunks == 1) return std::max<uint32_t>(32768u, B / 4u);
+        return std::max<uint32_t>(std::max<uint32_t>(32768u, std::min<uint32_t>(B / 64u, 262144u)), B / 256u);
+    }
     const uint32_t thr = c.opt_tail_paths > 0 ? (uint32_t)std::min<int64_t>(c.opt_tail_paths, 0xFFFFFFFFll) : 32768u;
     // B/256 with 288M-path pools (+0.9 % over B/128, profiles/r02/tail*/; B/128 was best with 96M pools)
     const uint32_t div = c.opt_tail_div > 0 ? (uint32_t)std::min<int64_t>(c.opt_tail_div, 0xFFFFFFFFll) : 256u;
@@ -1460,7 +1471,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
     // iteration (extend + shades + the survivor-count readback), or, below
     // the tail threshold, the tail kernel that finishes every remaining path.
     auto step = [&](Lane& L) -> int {
-        const uint32_t tail = tail_paths(*c, L.rp.B);
+        const uint32_t tail = tail_paths(*c, L.rp.B, nchunks, curve_kernel_scene(s->dev));
         if (L.n == 0) { L.state = Lane::DONE; return 0; }
         if (L.depth > kMaxDepth + 1) return fail("internal: path exceeded the depth cap");
         if (L.n <= tail) {
@@ -1572,7 +1583,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         rp.compact = compact ? 1u : 0u;
         rp.exact_libm = exact_libm ? 1u : 0u;
         HIPCHK(hipMemsetAsync(L.counts.p, 0, kIters * kCountsPerIter * sizeof(uint32_t), L.stream));
-        const uint32_t tail = tail_paths(*c, rp.B);
+        const uint32_t tail = tail_paths(*c, rp.B, nchunks, curve_kernel_scene(s->dev));
         L.fused_camera = s->cam_lds != 0 && rp.B > tail;     // the tail kernel starts from raygen's state
         if (!L.fused_camera) HIPCHK(launch_raygen(s->dev, rp, L.A, L.stream));
         L.cur = &L.A;
