@@ -2,6 +2,7 @@
 frame): C2's scene at NX x NY (default 1920x1080) and SPP per frame, timed over a few frames for each tail
 threshold (RT_OPT_TAIL_PATHS, 0 = the library's choice) given on the command line.
 Run on the GPU box: [NX=680 NY=381 FRAMES=3] python tools/small_frames.py SPP T1 T2 ..."""
+import hashlib
 import os
 import sys
 import time
@@ -37,5 +38,6 @@ for rnd in range(2):
         same = "ref" if ref is None else ("same" if (img == ref).all() else "DIFFERENT")
         if ref is None:
             ref = img
-        print("round %d spp %d tail_paths %d: %.3f ms/frame, %.0f Mrays/s (segments), image %s"
-              % (rnd, spp, tp, dt * 1e3, segs / frames / dt / 1e6, same), flush=True)
+        print("round %d spp %d tail_paths %d: %.3f ms/frame, %.0f Mrays/s (segments), image %s sha %s"
+              % (rnd, spp, tp, dt * 1e3, segs / frames / dt / 1e6, same,
+                 hashlib.sha256(img.tobytes()).hexdigest()[:16]), flush=True)
