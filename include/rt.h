@@ -74,7 +74,11 @@ int rt_context_release_pools(int ctx);
  *                     (setting it makes the next render size the pools again)
  *   RT_OPT_TAIL_PATHS a chunk with at most max(TAIL_PATHS, B / TAIL_DIV) live
  *   RT_OPT_TAIL_DIV   paths (B = the chunk's camera samples) finishes in the
- *                     persistent tail kernel; auto = 32768 and 256
+ *                     persistent tail kernel; with neither set the threshold
+ *                     follows the render: one chunk max(32768, B / 4), else
+ *                     max(32768, min(B / 64, 262144), B / 256) (curve-kernel
+ *                     scenes: max(32768, B / 256)); either set: the other's
+ *                     auto value is 32768 / 256
  *   RT_OPT_TAIL_OFF   nonzero: no tail kernel, every depth in the wavefront
  *                     kernels (tests and A/B runs)
  * One option selects arithmetic, not the schedule:
@@ -273,7 +277,7 @@ typedef struct rt_stats {
     double   ms_shade;    /* summed device time of the shade kernel */
     uint64_t extend_launches;
     uint64_t extend_rays; /* segments the extend kernels traced (the wavefront launches and the fused curve extend; the rest ran in the tail kernel) */
-    uint32_t max_depth_seen;  /* deepest wavefront iteration (the tail runs in k_finish) */
+    uint32_t max_depth_seen;  /* deepest wavefront iteration (the tail kernel and the fused curve extend run the deeper ones) */
     uint32_t reserved;
     double   ms_finish;       /* summed device time of the tail kernel */
     uint64_t finish_paths;    /* paths handed to the tail kernel */
