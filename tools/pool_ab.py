@@ -1,0 +1,30 @@
+"""C2 (cover 1920x1080x1024 spp) at a few path-pool sizes (RT_OPT_MAX_PATHS), variants interleaved:
+python tools/pool_ab.py M1 M2 ...  (millions of paths; 0 = the library's choice)."""
+import hashlib
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scheme-raytrace_amd"))
+from rtamd import gpu, scenes  # noqa: E402
+
+nx, ny, spp, seed = 1920, 1080, 1024, 0x5EED0002
+sc = scenes.random_scene(nx, ny)
+ctx = gpu.default_context()
+acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+for rnd in range(2):
+    for m in [int(x) for x in sys.argv[1:]]:
+        ctx.set_option("max_paths", m << 20)
+        gpu.render_device(sc, nx, ny, 0, 64, seed, acc.data_ptr())      # sizes the pools (warmup)
+        acc.zero_()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        h = gpu.render_device(sc, nx, ny, 0, spp, seed, acc.data_ptr())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        st = gpu.stats(h)
+        print("round %d max_paths %dM: %.1f ms, %.0f Mrays/s, chunks %d lanes %d, sha %s" % (
+            rnd, m, dt * 1e3, st.segments / dt / 1e6, st.chunks, st.lanes,
+            hashlib.sha256(acc.cpu().numpy().tobytes()).hexdigest()[:16]), flush=True)
