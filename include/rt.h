@@ -53,7 +53,7 @@ int rt_device_count(int* out_count);
 /* Context on one HIP device; owns a HIP stream and all device memory.
  * The render lanes' path pools belong to the context and are shared by every
  * scene rendered on it.  They are sized at the context's first render to
- * hold up to 288M paths, but at most 55 % of the device memory free at that
+ * hold up to 384Mi paths, but at most 65 % of the device memory free at that
  * moment (RT_OPT_MAX_PATHS overrides), and are kept for later renders;
  * rt_context_release_pools frees them (the next render sizes them again),
  * e.g. before the caller allocates large buffers of its own. */
@@ -69,8 +69,8 @@ int rt_context_release_pools(int ctx);
  *   RT_OPT_LANES      render lanes (path pool + stream) kept in flight, 1..4;
  *                     auto = 2, or 1 for scenes whose world BVH holds curves
  *                     (the persistent curve kernel fills the chip by itself)
- *   RT_OPT_MAX_PATHS  paths per pool (chunk of samples), >= 1024; auto = 288M,
- *                     at most 55 % of free device memory for the lanes together
+ *   RT_OPT_MAX_PATHS  paths per pool (chunk of samples), >= 1024; auto = 384Mi,
+ *                     at most 65 % of free device memory for the lanes together
  *                     (setting it makes the next render size the pools again)
  *   RT_OPT_TAIL_PATHS a chunk with at most max(TAIL_PATHS, B / TAIL_DIV) live
  *   RT_OPT_TAIL_DIV   paths (B = the chunk's camera samples) finishes in the

@@ -146,7 +146,7 @@ struct Lane {
 
 // A context owns the render lanes' path pools: every scene rendered on it
 // shares them (the C ABI renders one scene at a time per context), so a
-// second scene does not take a second 55 % of device memory.
+// second scene does not take a second 65 % of device memory.
 // The render schedule's knobs are options of the context (rt_context_set_option,
 // include/rt.h RT_OPT_*), 0 = the library's automatic choice.
 struct Context {
@@ -154,6 +154,7 @@ struct Context {
     hipStream_t stream = nullptr;
     DevBuf accum_tmp, img_tmp;
     size_t pool_cap = 0;                       // paths per chunk (max_paths), fixed at the first render
+    int pool_lanes = 0;                        // the lanes pool_cap was sized for
     std::unique_ptr<Lane> lanes[kLanes];       // rt_context_release_pools frees them
     int64_t opt_lanes = 0;                     // RT_OPT_LANES (0: 2, or 1 for curve-kernel scenes)
     int64_t opt_max_paths = 0;                 // RT_OPT_MAX_PATHS (0: sized from free memory)
@@ -1214,15 +1215,18 @@ std::string fault_text(uint32_t f) {
 // Path-pool cap (paths per chunk).  Bigger pools mean fewer chunks, each
 // with its own narrow tail: C2 (1920x1080x1024 spp) 13 383 Mrays/s with 96M
 // paths (22 chunks), 13 675 with 200M (12), 13 742 with 330M (8 chunks;
-// profiles/r02/pool/).  Default 288M paths, but at most what lets the render
-// lanes' pools (~272 B per path: two path-state pools, four hit queues, the
-// sample buffer) take 55 % of the device's free memory.  RT_OPT_MAX_PATHS overrides.
+// profiles/r02/pool/); round 5, with the first frame on new pools excluded (a re-allocated pool's first frame
+// waits for the driver to clear the memory it reuses, tools/realloc_probe.py): 8 chunks (288Mi- or 320Mi-path
+// cap) 13 804–13 888, 10 / 12 chunks 13 657–13 711, 6 chunks (354Mi) 13 927 / 13 957 (profiles/r05/ab/pool/).
+// Default 384Mi paths, but at most what lets the render lanes' pools (~272 B per path: two path-state
+// pools, four hit queues, the sample buffer) take 65 % of the device's free memory — on a 288-GB MI355X
+// C2's frame then cuts into 6 chunks (193 GB of pools).  RT_OPT_MAX_PATHS overrides.
 size_t max_paths(const Context& c, const int lanes) {
     if (c.opt_max_paths > 0) return c.opt_max_paths < 1024 ? 1024 : (size_t)c.opt_max_paths;
-    size_t v = (size_t)288 << 20;
+    size_t v = (size_t)384 << 20;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
-        const size_t fit = free_b / 100 * 55 / ((size_t)std::max(1, lanes) * 272);
+        const size_t fit = free_b / 100 * 65 / ((size_t)std::max(1, lanes) * 272);
         if (fit < v) v = fit;
     } else {
         (void)hipGetLastError();
@@ -1390,7 +1394,8 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         for (auto& L : c->lanes)
             if (L && L->stream) HIPCHK(hipStreamSynchronize(L->stream));
         for (auto& L : c->lanes) L.reset();
-        c->pool_cap = max_paths(*c, std::min(kLanes, lanes_wanted(*c)));
+        c->pool_lanes = std::min(kLanes, lanes_wanted(*c));
+        c->pool_cap = max_paths(*c, c->pool_lanes);
     }
     const size_t cap_paths = c->pool_cap;
     uint32_t chunk = (uint32_t)std::max<size_t>(1, cap_paths / npix);
@@ -1729,11 +1734,17 @@ int rt_context_set_option(int ctx, int option, int64_t value) {
     if (!c) return fail("invalid context handle");
     if (value < 0) return fail("option value must be >= 0 (0 = automatic)");
     switch (option) {
-    case RT_OPT_LANES:
+    case RT_OPT_LANES: {
         if (value > kLanes) return fail("RT_OPT_LANES: at most " + std::to_string(kLanes) + " render lanes");
-        if (value != c->opt_lanes) c->pool_cap = 0;   // the pools are sized for the lanes together: again
+        // more lanes than the pools were sized for: size them again for the lanes together (the next render
+        // frees them first); otherwise the lanes kept hold pools of the right size, so keep them — a re-allocated pool's
+        // first frame waits for the driver to clear the memory it reuses (4.7–6.6 s for C2's ~150 GB,
+        // profiles/r05/ab/realloc/), which a lane-count dip (bench.py's single-lane profiling frame) need not pay
+        const int64_t new_n = value > 0 ? std::min<int64_t>(value, kLanes) : 2;
+        if (new_n > c->pool_lanes) c->pool_cap = 0;
         c->opt_lanes = value;
         break;
+    }
     case RT_OPT_MAX_PATHS:
         if (value > ((int64_t)1 << 32)) return fail("RT_OPT_MAX_PATHS: at most 2^32 paths per pool");
         c->opt_max_paths = value;

@@ -334,7 +334,7 @@ def test_pools_shared_per_context_and_released(gpu_ctx, monkeypatch):
 
 
 def test_raising_lanes_resizes_pools():
-    """The path pools are sized at a render so that the lanes together take at most 55 % of the free
+    """The path pools are sized at a render so that the lanes together take at most 65 % of the free
     device memory.  Raising RT_OPT_LANES afterwards (2 -> 4) must size them again for four lanes (round-4
     advice: each extra lane used to allocate another pool of the two-lane size, ~110 % of the budget),
     and the image must not change."""

@@ -1,5 +1,6 @@
-"""C2 (cover 1920x1080x1024 spp) at a few path-pool sizes (RT_OPT_MAX_PATHS), variants interleaved:
-python tools/pool_ab.py M1 M2 ...  (millions of paths; 0 = the library's choice)."""
+"""C2 (cover 1920x1080x1024 spp) at a few path-pool sizes (RT_OPT_MAX_PATHS), variants interleaved; each
+size renders one untimed full frame first (a re-allocated pool's first frame waits for the driver to clear the
+memory it reuses: tools/realloc_probe.py): python tools/pool_ab.py M1 M2 ...  (millions; 0 = automatic)."""
 import hashlib
 import os
 import sys
@@ -17,7 +18,7 @@ acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
 for rnd in range(2):
     for m in [int(x) for x in sys.argv[1:]]:
         ctx.set_option("max_paths", m << 20)
-        gpu.render_device(sc, nx, ny, 0, 64, seed, acc.data_ptr())      # sizes the pools (warmup)
+        gpu.render_device(sc, nx, ny, 0, spp, seed, acc.data_ptr())     # sizes and first-touches the pools
         acc.zero_()
         torch.cuda.synchronize()
         t = time.perf_counter()
