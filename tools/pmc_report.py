@@ -70,7 +70,8 @@ def kernel_ms(d):
 def main():
     pdir, bench_log, out_path = sys.argv[1:4]
     from bench import EXTEND_BYTES_PER_PATH, EXTEND_BYTES_PER_SEGMENT, shade_bytes
-    d = json.loads([x for x in open(bench_log).read().splitlines() if x.startswith("{")][-1])
+    # the bench line (its start can share a log line with stderr output written around it)
+    d = json.loads([x[x.index('{"metric"'):] for x in open(bench_log).read().splitlines() if '{"metric"' in x][-1])
     steps = d["steps"]
     segs_wf = d["extend_rays_per_step"] * steps
     paths = d["paths_per_step"] * steps

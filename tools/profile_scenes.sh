@@ -1,10 +1,11 @@
 #!/bin/bash
 # Round-5 PMC profile sets for every benchmark scene (tools/profile_round.sh per scene), so each bench line
 # carries traffic / valu / valu_issue from profiles/pmc/<scene>_{extend,shade}.json (kernel-hash stamped).
-#   usage: tools/profile_scenes.sh TAG
+#   usage: tools/profile_scenes.sh TAG [SCENES]   (SCENES: a subset of "c2 c5 c3 c4 c4m", default all)
 set -o pipefail
 TAG=${1:-r05}
-run() { name=$1; shift; timeout -k 10 900 bash tools/profile_round.sh ${TAG}_$name "$@" > gpurun_out/prof_${TAG}_$name.log 2>&1 || { echo "profile $name failed"; tail -5 gpurun_out/prof_${TAG}_$name.log; exit 1; }; echo "profile $name ok"; }
+ONLY=${2:-"c2 c5 c3 c4 c4m"}
+run() { name=$1; shift; case " $ONLY " in *" $name "*) ;; *) return 0;; esac; timeout -k 10 900 bash tools/profile_round.sh ${TAG}_$name "$@" > gpurun_out/prof_${TAG}_$name.log 2>&1 || { echo "profile $name failed"; tail -5 gpurun_out/prof_${TAG}_$name.log; exit 1; }; echo "profile $name ok"; }
 mkdir -p gpurun_out
 run c2
 # C5 profiles the per-depth curve kernel the 256-spp configuration runs (a 4-spp frame would take the fused
