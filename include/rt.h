@@ -75,7 +75,8 @@ int rt_context_release_pools(int ctx);
  *   RT_OPT_TAIL_PATHS a chunk with at most max(TAIL_PATHS, B / TAIL_DIV) live
  *   RT_OPT_TAIL_DIV   paths (B = the chunk's camera samples) finishes in the
  *                     persistent tail kernel; with neither set the threshold
- *                     follows the render: one chunk max(32768, B / 4), else
+ *                     follows the render: one chunk max(32768,
+ *                     min(B / 4, 524288), B / 256), else
  *                     max(32768, min(B / 64, 262144), B / 256) (curve-kernel
  *                     scenes: max(32768, B / 256)); either set: the other's
  *                     auto value is 32768 / 256

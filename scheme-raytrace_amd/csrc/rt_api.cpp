@@ -1307,7 +1307,7 @@ bool curve_fuse(const DevScene& d, const uint32_t n) {
 // the tail kernel; RT_OPT_TAIL_OFF keeps every depth in the wavefront.
 // Without those options the threshold also follows the render's shape (round 5, C2's scene, same images;
 // profiles/r05/ab/tail/): a render of one chunk has no second lane to fill its narrow depths, so the tail
-// kernel takes over at B/4 (1 spp per frame, the progressive loop: 2.60 → 2.13 ms); renders of a few
+// kernel takes over at B/4, at most 524 288 paths (1 spp per frame, the progressive loop: 2.60 → 2.13 ms); renders of a few
 // small chunks take it at up to B/64, at most 262 144 paths (4 spp: 4.85 → 4.17 ms; 16 spp: 12.7 → 11.3 ms);
 // large chunks keep B/256 (the 8-GPU per-rank share, 680×381×1024 spp: 73.6 ms at B/256, 75.1 at B/64; C2:
 // B/256 over B/128, rounds 2–3).  Curve-kernel scenes keep the fixed rule (their tail kernel walks curves
@@ -1315,7 +1315,9 @@ bool curve_fuse(const DevScene& d, const uint32_t n) {
 uint32_t tail_paths(const Context& c, const uint32_t B, const int nchunks, const bool curves) {
     if (c.wavefront_only) return 0u;
     if (c.opt_tail_paths <= 0 && c.opt_tail_div <= 0 && !curves) {
-        if (nchunks == 1) return std::max<uint32_t>(32768u, B / 4u);
+        // (bounded: a large single chunk — one render lane, e.g. Cornell at 256 spp, 268M paths — keeps B/256;
+        // B/4 there handed a quarter of the paths to the tail kernel: 100.6 of 213 ms)
+        if (nchunks == 1) return std::max<uint32_t>(std::max<uint32_t>(32768u, std::min<uint32_t>(B / 4u, 524288u)), B / 256u);
         return std::max<uint32_t>(std::max<uint32_t>(32768u, std::min<uint32_t>(B / 64u, 262144u)), B / 256u);
     }
     const uint32_t thr = c.opt_tail_paths > 0 ? (uint32_t)std::min<int64_t>(c.opt_tail_paths, 0xFFFFFFFFll) : 32768u;
