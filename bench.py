@@ -9,7 +9,7 @@ integrator).  `value` = total segments / wall time over
 the timed steps (max over ranks), inputs resident in HBM.
 
 Multi-GPU (torch.distributed.run, one process per GPU): the frame is split
-into interleaved 16x16 tiles (tile (tx, ty) -> rank (tx + 3 ty) % N); each rank renders its
+into interleaved 16x16 tiles (tile (tx, ty) -> rank (tx + k ty) % N, k = 3, or 5 when 3 | N); each rank renders its
 tiles into a compact accumulator of its own pixels (rt_render_shard_device)
 and rank 0 gathers the shards over RCCL / xGMI at frame end and scatters them
 into the frame (rtamd.dist.gather_frame; the pixels are disjoint, so the
@@ -325,7 +325,7 @@ def gpu_band_parity(scene, nx, ny, seed, ref, h, ctx):
 
 
 def shard_balance(a, scene, h, ctx, nx, ny, spp, counts):
-    """--shard-balance: the multi-GPU frame's tile shards (rt_render_shard_device, tile (tx, ty) -> shard (tx + 3 ty) % N)
+    """--shard-balance: the multi-GPU frame's tile shards (rt_render_shard_device, tile (tx, ty) -> shard (tx + k ty) % N)
     rendered one at a time on this GPU, each timed alone, against the whole frame rendered the same way.
     max / mean of the shard times bounds N-GPU strong-scaling efficiency (the frame waits for its slowest
     rank); T_frame / max(T_shard) is the speedup the partition allows before the gather."""

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* Sky functions (scene slot 4, geometry.scm:30-31).  The reference stores an
  * arbitrary closure; the two it defines are sky-color (main.scm:91-95) and
@@ -68,7 +68,12 @@ int rt_context_release_pools(int ctx);
  * accumulation).
  *   RT_OPT_LANES      render lanes (path pool + stream) kept in flight, 1..4;
  *                     auto = 2, or 1 for scenes whose world BVH holds curves
- *                     (the persistent curve kernel fills the chip by itself)
+ *                     (the persistent curve kernel fills the chip by itself);
+ *                     raising it above the lanes the pools were sized for
+ *                     sizes them again at the next render, lowering it keeps
+ *                     the pools as they are (each lane then holds the smaller
+ *                     per-lane share of the larger count; RT_OPT_MAX_PATHS or
+ *                     rt_context_release_pools resizes them)
  *   RT_OPT_MAX_PATHS  paths per pool (chunk of samples), >= 1024; auto = 384Mi,
  *                     at most 65 % of free device memory for the lanes together
  *                     (setting it makes the next render size the pools again)
@@ -181,8 +186,9 @@ int rt_scene_commit(int scene, int world_list_obj);
  * rt_render_device: accum is caller-owned DEVICE memory on the context's GPU
  * (e.g. a torch tensor's data_ptr); stream is a hipStream_t or NULL for the
  * context's own stream.  shard_index/shard_count select an interleaved subset
- * of 16x16 pixel tiles (tile (tx, ty) belongs to shard (tx + 3 ty) % shard_count); pixels of
- * other shards are left untouched. */
+ * of 16x16 pixel tiles (tile (tx, ty) belongs to shard (tx + k ty) % shard_count, k the
+ * smallest odd prime that does not divide shard_count: 3, or 5 for 3, 6, 9, ... shards);
+ * pixels of other shards are left untouched. */
 int rt_render(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
               double* accum_host);
 int rt_render_device(int scene, int nx, int ny, int spp_begin, int spp_count, uint64_t seed,
@@ -213,9 +219,10 @@ int rt_render_shard_device(int scene, int nx, int ny, int spp_begin, int spp_cou
 
 /* The pixels shard `shard_index` of `shard_count` renders (host-only, no GPU
  * needed): interleaved 16x16 tiles in row-major tile order, tile (tx, ty)
- * belongs to shard (tx + 3 ty) % shard_count (diagonal, so no shard gets whole
- * columns); pixel j = y*nx + x, listed tile by tile.  Pass
- * out_pix = NULL to get the count only. */
+ * belongs to shard (tx + k ty) % shard_count, k = the smallest odd prime not
+ * dividing shard_count (diagonal and coprime, so no shard gets whole columns
+ * or only some residues of them); pixel j = y*nx + x, listed tile by tile.
+ * Pass out_pix = NULL to get the count only. */
 int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* out_pix, int64_t* out_count);
 
 /* ---- multi-GPU frame (one process per GPU) ----------------
@@ -238,12 +245,26 @@ int rt_shard_pixels(int nx, int ny, int shard_index, int shard_count, uint32_t* 
  *   overwritten.  Enqueued on `stream` (NULL: the context's stream), which the
  *   call synchronises before it returns.  The frame equals a one-process
  *   rt_render_device of the same passes bit for bit (disjoint pixels, nothing
- *   is summed). */
+ *   is summed).  The communicator stays valid through the call even if another
+ *   thread destroys its handle; its context must outlive the call.
+ * rt_gather_layout: host-only (no GPU, no RCCL): for each rank r of `world`,
+ *   out_count[r] = its shard's pixel count and out_offset[r] = the offset of
+ *   its pixels in the ranks' concatenated rt_shard_pixels lists (out_offset[0]
+ *   = 0).  Rank 0 receives rank r's compact accumulator at doubles
+ *   3 * (out_offset[r] - out_count[0]) of its receive buffer.
+ * rt_gather_shards_local: the same gather within one process (every shard of
+ *   `world` on the context's device, e.g. several shards rendered by one
+ *   GPU): accum_compact = a host array of `world` device pointers, shard r's
+ *   compact accumulator in entry r; the same receive layout and placement as
+ *   rt_gather_shards, with device copies in place of the sends and receives. */
 #define RT_COMM_ID_BYTES 128
 int rt_comm_unique_id(uint8_t out_id[RT_COMM_ID_BYTES]);
 int rt_comm_create(int ctx, const uint8_t unique_id[RT_COMM_ID_BYTES], int rank, int world, int* out_comm);
 int rt_comm_destroy(int comm);
 int rt_gather_shards(int comm, int nx, int ny, const double* accum_compact, double* frame_device, void* stream);
+int rt_gather_layout(int nx, int ny, int world, int64_t* out_count, int64_t* out_offset);
+int rt_gather_shards_local(int ctx, int nx, int ny, int world, const double* const* accum_compact,
+                           double* frame_device, void* stream);
 
 /* Errors raised on the device.  Every loop of the kernels that waits on data
  * (rejection samplers, curve subdivision walks, persistent kernels' per-path

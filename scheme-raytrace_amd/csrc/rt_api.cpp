@@ -23,8 +23,7 @@
 namespace rtamd {
 hipError_t launch_raygen(const DevScene&, const RenderParams&, const PathState&, hipStream_t);
 hipError_t launch_extend(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
-                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, const CurveSplit*, const CurveFuse*,
-                         hipStream_t);
+                         const HitBuf&, uint32_t, uint32_t*, bool, unsigned int*, const CurveFuse*, hipStream_t);
 hipError_t launch_shade(int, const DevScene&, const DevScene*, const RenderParams&, const PathState&, const HitBuf&,
                         const QView&, uint32_t, const PathState&, uint32_t*, uint32_t, uint32_t, hipStream_t);
 hipError_t launch_finish(const DevScene&, const DevScene*, const RenderParams&, const PathState&, const QView&, uint32_t,
@@ -40,7 +39,6 @@ hipError_t launch_extend_lds(const DevScene&, const RenderParams&, const PathSta
                              const HitBuf&, uint32_t, uint32_t*, uint32_t, unsigned long long*, hipStream_t);
 hipError_t launch_resolve_u8(const double*, uint32_t, int, uint8_t*, hipStream_t);
 hipError_t launch_scatter_pixels(const double*, const uint32_t*, uint32_t, double*, hipStream_t);
-bool curve_split();
 bool curve_persistent();
 hipError_t launch_curve_depth(const double*, const double*, uint32_t, int32_t*, hipStream_t);
 hipError_t take_fault(uint32_t*);
@@ -102,23 +100,10 @@ struct DevBuf {
 // long, narrow tail of one chunk (its last few paths bouncing to depth 100)
 // overlaps the wide first iterations of the next one instead of leaving the
 // chip mostly idle.  Accumulation stays in chunk (= sample) order.
-#ifndef RT_CURVE_K
-#define RT_CURVE_K 32
-#endif
-#ifndef RT_TRAV_LDS_STACK
-#define RT_TRAV_LDS_STACK 24           // k_curve_trav's LDS stack column (rt_kernels.hip, the same default)
-#endif
-constexpr int RT_TRAV_LDS_STACK_HOST = RT_TRAV_LDS_STACK;
-#ifndef RT_CURVE_LIST_WAVES
-#define RT_CURVE_LIST_WAVES 2          // k_extend_curves<true>'s waves per SIMD (rt_kernels.hip, the same default)
-#endif
-constexpr int RT_CURVE_LIST_WAVES_HOST = RT_CURVE_LIST_WAVES;
 constexpr int kLanes = 4;                  // most lanes a render may use (RT_OPT_LANES)
 constexpr int kCurveLdsStack = RT_CURVE_LDS_STACK;   // k_extend_curves' BVH4 stack entries in LDS per lane
 struct Lane {
     DevBuf st_a, st_b, hit, sb, counts, seg_tail;
-    DevBuf cw_buf;                             // the split curve extend's per-ray buffers (curve scenes)
-    CurveSplit cs{};
     uint32_t* h_counts = nullptr;              // pinned survivor counts, one row per iteration
     hipStream_t stream = nullptr;
     hipEvent_t ev_cnt = nullptr;               // the last iteration's survivor counts are on the host
@@ -144,6 +129,21 @@ struct Lane {
     }
 };
 
+// The frame-end gather's layout for one frame size and world (rt_gather_layout): per rank its shard's
+// pixel count and the offset of its pixels in the ranks' concatenated pixel lists (rt_shard_pixels order,
+// ranks in order).  The root (rank 0) also keeps that concatenated list on the device and a receive
+// buffer for the other ranks' compact accumulators: rank r's lands at doubles recv_at(r).  Both gathers —
+// over RCCL (rt_gather_shards) and within one process (rt_gather_shards_local) — fill it the same way and
+// place it with the same kernel (gather_place).
+struct GatherPlan {
+    int nx = -1, ny = -1, world = 0;
+    bool root = false;
+    std::vector<int64_t> count, off;
+    DevBuf pix, recv;
+    size_t recv_at(int r) const { return 3 * (size_t)(off[r] - count[0]); }
+    int64_t others() const { return off[world - 1] + count[world - 1] - count[0]; }
+};
+
 // A context owns the render lanes' path pools: every scene rendered on it
 // shares them (the C ABI renders one scene at a time per context), so a
 // second scene does not take a second 65 % of device memory.
@@ -161,6 +161,7 @@ struct Context {
     int64_t opt_tail_paths = 0;                // RT_OPT_TAIL_PATHS (0: 32768)
     int64_t opt_tail_div = 0;                  // RT_OPT_TAIL_DIV (0: 256)
     bool wavefront_only = false;               // RT_OPT_TAIL_OFF: no tail kernel (tests, A/B)
+    GatherPlan gplan;                          // rt_gather_shards_local's plan (the frame size last gathered)
     int64_t opt_exact_libm = RT_LIBM_AUTO;     // RT_OPT_EXACT_LIBM: the bounce directions' sin / cos
 };
 
@@ -199,21 +200,20 @@ struct Scene {
 };
 
 // A multi-GPU frame's communicator (rt_comm_create): one RCCL rank per process, bound to a context's
-// device.  Rank 0 keeps every rank's pixel list (rt_shard_pixels order, ranks concatenated) and a receive
-// buffer for the other ranks' compact accumulators, both kept for the frame size last gathered.
+// device.  The gather's plan is kept for the frame size last gathered.
 struct Comm {
     int ctx = -1, rank = 0, world = 1;
+    int device = 0;
     ncclComm_t nc = nullptr;
-    int nx = -1, ny = -1;
-    std::vector<int64_t> count, off;               // per rank: shard pixels and their offset in the lists
-    DevBuf pix, recv;
+    GatherPlan plan;
     ~Comm() { if (nc) (void)ncclCommDestroy(nc); }
 };
 
 std::mutex g_mu;
 std::map<int, std::unique_ptr<Context>> g_ctx;
 std::map<int, std::unique_ptr<Scene>> g_scene;
-std::map<int, std::unique_ptr<Comm>> g_comm;
+// shared: rt_gather_shards keeps its communicator alive outside the lock (it waits for the other ranks)
+std::map<int, std::shared_ptr<Comm>> g_comm;
 int g_next_ctx = 1, g_next_scene = 1, g_next_comm = 1;
 
 Context* get_ctx(int h) {
@@ -1064,7 +1064,6 @@ int commit_scene(Scene* s, int world) {
     }
     d.n_bleaf = (int)bleaf.size();
     d.lane_stack = lane_stack;
-    for (const BvhLeaf& L : bleaf) d.max_leaf_bez = std::max(d.max_leaf_bez, L.bn);
     if (lane_stack > kLaneStack) return fail("internal: BVH deeper than the traversal stack");
     if (!bvh4.empty()) {
         if (int rc = upload(s->d_bvh4, bvh4, &d.bvh4)) return rc;
@@ -1080,7 +1079,7 @@ int commit_scene(Scene* s, int world) {
             int dev = 0, cus = 0;
             HIPCHK(hipGetDevice(&dev));
             HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * (uint32_t)std::max(RT_CURVE_WAVES, RT_CURVE_LIST_WAVES_HOST);
+            d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * (uint32_t)RT_CURVE_WAVES;
             HIPCHK(s->d_bez_ring.ensure((size_t)kLanes * d.ring_waves * kBezRing * 128u));
             d.bez_ring = s->d_bez_ring.as<double>();
         }
@@ -1183,23 +1182,67 @@ int commit_scene(Scene* s, int world) {
 // t % nshard).  Listed tile by tile, pixel j = y*nx + x.
 struct PixSel { int y0, y1, shard, nshard; };
 PixSel full_frame(int ny) { return PixSel{0, ny, 0, 1}; }
+// The diagonal tile deal's row stride: the smallest odd prime coprime with the shard count (3 for every
+// count not divisible by 3, so 1, 2, 4 and 8 shards keep the round-5 deal; 5 for 3 or 6 shards).  With a
+// stride sharing a factor with the count, shard r would only ever get the columns tx = r mod that factor.
+int tile_stride(const int nshard) {
+    for (int k : {3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
+        if (nshard % k != 0) return k;
+    return 37;                               // a product of the primes to 31 exceeds any int shard count
+}
 std::vector<uint32_t> make_pixlist(int nx, int ny, const PixSel& ps) {
     const int T = 16;
     const int tx = (nx + T - 1) / T, ty = (ny + T - 1) / T;
     std::vector<uint32_t> out;
     out.reserve((size_t)nx * (size_t)(ps.y1 - ps.y0) / (size_t)ps.nshard + T * T);
-    // tile (x, y) belongs to shard (x + 3 y) % nshard.  Plain t % nshard degenerates into vertical 16-px
-    // stripes whenever nshard divides the tiles per row (C2: 120, C4: 64): every rank then renders the same
-    // columns of every row, and the Cornell box's walls are not alike (shard balance at C4, one GPU per
-    // shard: max / mean 1.0385 for 8 shards, 1.0247 for 4; profiles/r05/balance.log).  The diagonal deal
-    // gives every shard one tile of each 8 consecutive ones along a row and along a column.
+    // tile (x, y) belongs to shard (x + k y) % nshard, k = tile_stride(nshard).  Plain t % nshard degenerates
+    // into vertical 16-px stripes whenever nshard divides the tiles per row (C2: 120, C4: 64): every rank then
+    // renders the same columns of every row, and the Cornell box's walls are not alike (shard balance at C4,
+    // one GPU per shard: max / mean 1.0385 for 8 shards, 1.0247 for 4; profiles/r05/balance.log).  The
+    // diagonal deal with k coprime to nshard gives every shard one tile of each nshard consecutive ones along
+    // a row and along a column.
+    const int k = tile_stride(ps.nshard);
     for (int t = 0; t < tx * ty; ++t) {
-        if (((t % tx) + 3 * (t / tx)) % ps.nshard != ps.shard) continue;
+        if (((t % tx) + k * (t / tx)) % ps.nshard != ps.shard) continue;
         const int bx = (t % tx) * T, by = (t / tx) * T;
         for (int yy = std::max(by, ps.y0); yy < std::min(std::min(by + T, ny), ps.y1); ++yy)
             for (int xx = bx; xx < std::min(bx + T, nx); ++xx) out.push_back((uint32_t)(yy * nx + xx));
     }
     return out;
+}
+
+// (re)build the gather plan for a frame size and world; the root's device list and receive buffer too
+int gather_plan(GatherPlan& g, int nx, int ny, int world, bool root) {
+    if (g.nx == nx && g.ny == ny && g.world == world && g.root == root) return 0;
+    g.nx = -1;
+    g.world = world;
+    g.root = root;
+    g.count.assign(world, 0);
+    g.off.assign(world, 0);
+    std::vector<uint32_t> all;
+    int64_t total = 0;
+    for (int r = 0; r < world; ++r) {
+        const std::vector<uint32_t> pl = make_pixlist(nx, ny, PixSel{0, ny, r, world});
+        g.off[r] = total;
+        g.count[r] = (int64_t)pl.size();
+        total += g.count[r];
+        if (root) all.insert(all.end(), pl.begin(), pl.end());
+    }
+    if (root) {
+        HIPCHK(g.pix.ensure(std::max<size_t>(1, all.size()) * sizeof(uint32_t)));
+        if (!all.empty()) HIPCHK(hipMemcpy(g.pix.p, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        HIPCHK(g.recv.ensure(std::max<size_t>(1, (size_t)g.others()) * 3 * sizeof(double)));
+    }
+    g.nx = nx;
+    g.ny = ny;
+    return 0;
+}
+// the root's placement: its own compact accumulator, then the received shards, into the y-up frame
+int gather_place(const GatherPlan& g, const double* own, double* frame, hipStream_t st) {
+    const uint32_t* pix = g.pix.as<const uint32_t>();
+    if (g.count[0] > 0) HIPCHK(launch_scatter_pixels(own, pix, (uint32_t)g.count[0], frame, st));
+    HIPCHK(launch_scatter_pixels(g.recv.as<const double>(), pix + g.count[0], (uint32_t)g.others(), frame, st));
+    return 0;
 }
 
 std::string fault_text(uint32_t f) {
@@ -1241,41 +1284,6 @@ int lanes_wanted(const Context& c) {   // RT_OPT_LANES: path pools kept in fligh
 bool curve_kernel_scene(const DevScene& d) {
     return d.n_bez > 0 && d.bvh_has_bez && d.bez_groups == 0 && d.n_med == 0 && d.n_klein == 0;
 }
-// The split curve extend's per-ray buffers of a lane (rays per slice: at most 16M and the lane's pool):
-// closest 8 B, best 4, list length 4, K candidates of 8 B, the save area (S words), two continuation lists
-hipError_t ensure_curve_split(Lane& L, const DevScene& d, const size_t pool) {
-    // RTAMD_CURVE_K (tests): shorter lists, so rays continue over many rounds (k_curve_trav<true>)
-    const char* ke = std::getenv("RTAMD_CURVE_K");
-    const uint32_t K = (uint32_t)std::max(ke ? std::atoi(ke) : RT_CURVE_K, d.max_leaf_bez + 4);
-    const uint32_t S = (uint32_t)std::max(d.stack4, d.lds4) + 2u;
-    const uint32_t cap = (uint32_t)std::min<size_t>(pool, (size_t)16 << 20);
-    const size_t per = 8 + 4 + 4 + (size_t)K * 8 + (size_t)S * 4 + 2 * 4;
-    const char* le0 = std::getenv("RTAMD_CURVE_LDS_STACK");
-    const int lds = std::min(RT_TRAV_LDS_STACK_HOST, le0 ? std::max(1, std::atoi(le0)) : RT_TRAV_LDS_STACK_HOST);
-    if (L.cs.cap >= cap && L.cs.w.K == K && L.cs.w.S == S) { L.cs.w.lds = lds; return hipSuccess; }
-    const hipError_t e = L.cw_buf.ensure((size_t)cap * per + 2 * 256);
-    if (e != hipSuccess) return e;
-    char* p = L.cw_buf.as<char>();
-    CurveSplit cs{};
-    cs.w.closest = reinterpret_cast<double*>(p); p += (size_t)cap * 8;
-    cs.w.cand = reinterpret_cast<CurveCand*>(p); p += (size_t)cap * K * 8;
-    cs.w.best = reinterpret_cast<int32_t*>(p); p += (size_t)cap * 4;
-    cs.w.ncand = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
-    cs.w.save = reinterpret_cast<int32_t*>(p); p += (size_t)cap * S * 4;
-    cs.cont[0] = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
-    cs.cont[1] = reinterpret_cast<uint32_t*>(p); p += (size_t)cap * 4;
-    cs.cnt[0] = reinterpret_cast<uint32_t*>(p); p += 256;
-    cs.cnt[1] = reinterpret_cast<uint32_t*>(p);
-    cs.w.K = K;
-    cs.w.S = S;
-    // RTAMD_CURVE_LDS_STACK (tests): fewer LDS entries, so the walk's deeper entries take the save area
-    const char* le = std::getenv("RTAMD_CURVE_LDS_STACK");
-    cs.w.lds = std::min(RT_TRAV_LDS_STACK_HOST, le ? std::max(1, std::atoi(le)) : RT_TRAV_LDS_STACK_HOST);
-    cs.cap = cap;
-    L.cs = cs;
-    return hipSuccess;
-}
-
 // Scenes whose world BVH holds curves run the persistent curve kernel, whose
 // grid fills the chip by itself: a second lane's kernels only queue behind it
 // and its narrow tails, so one lane is faster (C5 at 64 spp: 200.3 vs 164.1
@@ -1448,8 +1456,6 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         // tail segments, next tail path / curve claim, LDS errors, the fused curve extend's continuation segments
         HIPCHK(L.seg_tail.ensure(4 * sizeof(unsigned long long)));
         if (!L.h_counts) HIPCHK(hipHostMalloc((void**)&L.h_counts, kIters * kCountsPerIter * sizeof(uint32_t)));
-        if (curve_kernel_scene(s->dev) && curve_split()) HIPCHK(ensure_curve_split(L, s->dev, cap));
-        else if (L.cs.cap) { L.cs = CurveSplit{}; L.cw_buf.release(); }   // (the previous render drained the lane)
         HIPCHK(hipStreamWaitEvent(L.stream, ev_in, 0));
         HIPCHK(hipMemsetAsync(L.seg_tail.p, 0, 4 * sizeof(unsigned long long), L.stream));
         L.A = carve_state(L.st_a.p, scap);
@@ -1518,11 +1524,11 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             if (dl.bez_ring) dl.bez_ring += (size_t)L.index * dl.ring_waves * kBezRing * 16u;
             // the fused curve extend (k_extend_curves<FUSE>): every depth from 1 on in this one launch
             CurveFuse fz{L.seg_tail.as<unsigned long long>() + 3, (uint32_t)L.depth};
-            fused = L.depth > 0 && curve_fuse(s->dev, L.n) && !(L.cs.cap && curve_split());
+            fused = L.depth > 0 && curve_fuse(s->dev, L.n);
             HIPCHK(launch_extend(dl, s->d_dev.as<const DevScene>(), L.rp, *L.cur, L.view, L.n, hit,
                                  (uint32_t)shard_cap, cnt, L.depth == 0,
                                  reinterpret_cast<unsigned int*>(L.seg_tail.as<unsigned long long>() + 1),
-                                 L.cs.cap ? &L.cs : nullptr, fused ? &fz : nullptr, L.stream));
+                                 fused ? &fz : nullptr, L.stream));
         }
         if (s->profiling) HIPCHK(hipEventRecord(L.ev[1], L.stream));
         uint32_t* surv = cnt + 4 * kShards * kCntStride;
@@ -1568,9 +1574,11 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         L.view = QView{L.counts.as<uint32_t>() + L.depth * kCountsPerIter + 4 * kShards * kCntStride,
                        (uint32_t)shard_cap};
         std::swap(L.cur, L.nxt);
-        static const bool dbg_depth = std::getenv("RTAMD_DEBUG_DEPTH") != nullptr;   // diagnostics: live paths per depth
+#ifdef RT_STATS
+        static const bool dbg_depth = std::getenv("RTAMD_DEBUG_DEPTH") != nullptr;   // stats builds: live paths per depth
         if (dbg_depth) std::fprintf(stderr, "depth-count lane %d chunk %d depth %d in %u out %u\n", L.index, L.chunk,
                                     L.depth, L.n, n);
+#endif
         L.n = n;
         ++L.depth;
         return step(L);
@@ -2326,8 +2334,8 @@ int rt_comm_create(int ctx, const uint8_t unique_id[RT_COMM_ID_BYTES], int rank,
     HIPCHK(hipSetDevice(device));
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof id);
-    auto m = std::make_unique<Comm>();
-    m->ctx = ctx; m->rank = rank; m->world = world;
+    auto m = std::make_shared<Comm>();
+    m->ctx = ctx; m->rank = rank; m->world = world; m->device = device;
     // collective: returns once every rank has called it (outside the lock: it waits for the other processes)
     NCCLCHK(ncclCommInitRank(&m->nc, world, id, rank));
     std::lock_guard<std::mutex> lk(g_mu);
@@ -2350,61 +2358,82 @@ int rt_comm_destroy(int comm) {
 int rt_gather_shards(int comm, int nx, int ny, const double* accum_compact, double* frame_device, void* stream) {
     if (nx <= 0 || ny <= 0) return fail("image size must be positive");
     if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
-    Comm* m = nullptr;
-    Context* c = nullptr;
+    std::shared_ptr<Comm> keep;                       // alive through the call, whatever rt_comm_destroy does
+    hipStream_t st = (hipStream_t)stream;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_comm.find(comm);
         if (it == g_comm.end()) return fail("invalid communicator handle");
-        m = it->second.get();
-        c = get_ctx(m->ctx);
+        keep = it->second;
+        Context* c = get_ctx(keep->ctx);
         if (!c) return fail("the communicator's context was destroyed");
+        if (!st) st = c->stream;                      // (the context must outlive the call: rt.h)
     }
-    HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    if (m->nx != nx || m->ny != ny) {                  // the shards' pixel lists for this frame size
-        m->nx = -1;
-        m->count.assign(m->world, 0);
-        m->off.assign(m->world, 0);
-        std::vector<uint32_t> all;
-        for (int r = 0; r < m->world; ++r) {
-            const std::vector<uint32_t> pl = make_pixlist(nx, ny, PixSel{0, ny, r, m->world});
-            m->off[r] = (int64_t)all.size();
-            m->count[r] = (int64_t)pl.size();
-            if (m->rank == 0) all.insert(all.end(), pl.begin(), pl.end());
-        }
-        if (m->rank == 0) {
-            HIPCHK(m->pix.ensure(std::max<size_t>(1, all.size()) * sizeof(uint32_t)));
-            HIPCHK(hipMemcpy(m->pix.p, all.data(), all.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-            const size_t others = all.size() - (size_t)m->count[0];
-            HIPCHK(m->recv.ensure(std::max<size_t>(1, others) * 3 * sizeof(double)));
-        }
-        m->nx = nx; m->ny = ny;
-    }
-    const int64_t mine = m->count[m->rank];
+    Comm* m = keep.get();
+    HIPCHK(hipSetDevice(m->device));
+    if (int rc = gather_plan(m->plan, nx, ny, m->world, m->rank == 0)) return rc;
+    const GatherPlan& g = m->plan;
+    const int64_t mine = g.count[m->rank];
     if (mine > 0 && !accum_compact) return fail("null compact accumulator");
     if (m->rank == 0 && !frame_device) return fail("rank 0 needs the frame buffer");
     // RCCL has no gather: every other rank sends its compact accumulator (its exact size, no padding) to
-    // rank 0, which posts one receive per rank into its buffer, in one group
+    // rank 0, which posts one receive per rank into its buffer at recv_at(r), in one group.
+    // The group is always closed, also after a failed call inside it (an open group poisons the thread's
+    // later RCCL calls).
     if (m->world > 1) {
-        NCCLCHK(ncclGroupStart());
+        ncclResult_t r0 = ncclGroupStart();
+        if (r0 != ncclSuccess) return fail(std::string("ncclGroupStart: ") + ncclGetErrorString(r0));
+        ncclResult_t bad = ncclSuccess;
         if (m->rank != 0) {
-            if (mine > 0) NCCLCHK(ncclSend(accum_compact, (size_t)(3 * mine), ncclDouble, 0, m->nc, st));
+            if (mine > 0) bad = ncclSend(accum_compact, (size_t)(3 * mine), ncclDouble, 0, m->nc, st);
         } else {
-            double* recv = m->recv.as<double>();
-            for (int r = 1; r < m->world; ++r)
-                if (m->count[r] > 0)
-                    NCCLCHK(ncclRecv(recv + 3 * (m->off[r] - m->count[0]), (size_t)(3 * m->count[r]), ncclDouble, r,
-                                     m->nc, st));
+            double* recv = g.recv.as<double>();
+            for (int r = 1; r < m->world && bad == ncclSuccess; ++r)
+                if (g.count[r] > 0) bad = ncclRecv(recv + g.recv_at(r), (size_t)(3 * g.count[r]), ncclDouble, r, m->nc, st);
         }
-        NCCLCHK(ncclGroupEnd());
+        const ncclResult_t end = ncclGroupEnd();
+        if (bad != ncclSuccess) return fail(std::string("ncclSend / ncclRecv: ") + ncclGetErrorString(bad));
+        if (end != ncclSuccess) return fail(std::string("ncclGroupEnd: ") + ncclGetErrorString(end));
     }
-    if (m->rank == 0) {                                // place every shard's pixels into the y-up frame
-        const uint32_t* pix = m->pix.as<const uint32_t>();
-        HIPCHK(launch_scatter_pixels(accum_compact, pix, (uint32_t)m->count[0], frame_device, st));
-        const int64_t others = m->off[m->world - 1] + m->count[m->world - 1] - m->count[0];
-        HIPCHK(launch_scatter_pixels(m->recv.as<const double>(), pix + m->count[0], (uint32_t)others, frame_device, st));
-    }
+    if (m->rank == 0)                                  // place every shard's pixels into the y-up frame
+        if (int rc = gather_place(g, accum_compact, frame_device, st)) return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int rt_gather_layout(int nx, int ny, int world, int64_t* out_count, int64_t* out_offset) {
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
+    if (world <= 0) return fail("invalid world size");
+    if (!out_count || !out_offset) return fail("null out pointer");
+    GatherPlan g;
+    if (int rc = gather_plan(g, nx, ny, world, false)) return rc;
+    for (int r = 0; r < world; ++r) { out_count[r] = g.count[r]; out_offset[r] = g.off[r]; }
+    return 0;
+}
+
+int rt_gather_shards_local(int ctx, int nx, int ny, int world, const double* const* accum_compact,
+                           double* frame_device, void* stream) {
+    if (nx <= 0 || ny <= 0) return fail("image size must be positive");
+    if ((uint64_t)nx * (uint64_t)ny >= (1ull << 31)) return fail("image too large");
+    if (world <= 0) return fail("invalid world size");
+    if (!accum_compact || !frame_device) return fail("null pointer");
+    std::lock_guard<std::mutex> lk(g_mu);
+    Context* c = get_ctx(ctx);
+    if (!c) return fail("invalid context handle");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (int rc = gather_plan(c->gplan, nx, ny, world, true)) return rc;
+    const GatherPlan& g = c->gplan;
+    for (int r = 0; r < world; ++r)
+        if (g.count[r] > 0 && !accum_compact[r]) return fail("null compact accumulator for shard " + std::to_string(r));
+    // what the RCCL gather's receives do: shard r's compact accumulator at recv_at(r)
+    double* recv = g.recv.as<double>();
+    for (int r = 1; r < world; ++r)
+        if (g.count[r] > 0)
+            HIPCHK(hipMemcpyAsync(recv + g.recv_at(r), accum_compact[r], (size_t)g.count[r] * 3 * sizeof(double),
+                                  hipMemcpyDeviceToDevice, st));
+    if (int rc = gather_place(g, accum_compact[0], frame_device, st)) return rc;
     HIPCHK(hipStreamSynchronize(st));
     return 0;
 }

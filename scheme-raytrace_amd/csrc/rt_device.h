@@ -163,7 +163,6 @@ struct DevScene {
     double* bez_ring;  uint32_t ring_waves;
     int32_t bvh4_root, stack4;
     int32_t lds4;                                  // the walk's stack entries in LDS (lane_stack; tests lower it)
-    int32_t max_leaf_bez;                          // most curves in one BvhLeaf (k_curve_trav lists a leaf at once)
     uint32_t* stk_ovf;     uint32_t ovf_lanes;
     // Time-0 tree over the same primitives (nullptr = none): every moving
     // sphere frozen at center(0), so rays with time +0.0 (all scattered rays,
@@ -248,38 +247,11 @@ constexpr int kShards = 8;
 constexpr int kCntStride = RT_CNT_STRIDE;
 struct QView { const uint32_t* counts; uint32_t cap; };
 
-// The split curve extend (round 5): k_curve_trav walks the BVH4 for each ray of a slice of the launch's
-// ray list and leaves a list of curve candidates; k_extend_curves<true> tests them (rt_kernels.hip).
-// Per-ray buffers of one render lane, for ray k of the slice (ray queue index k0 + k):
-struct alignas(8) CurveCand { uint32_t curve, tn; };   // curve index, f32 bits of its box's entry t (0: tested)
-struct CurveWork {
-    double* closest;          // closest t so far (the groups before the BVH, sphere leaves, curve results)
-    int32_t* best;            // its leaf id (-1: none)
-    uint32_t* ncand;          // candidates listed this round; bit 31: the traversal goes on (the list was full)
-    CurveCand* cand;          // K per ray, in traversal order
-    int32_t* save;            // S per ray: a continuing traversal's next node, its stack depth and entries
-    const uint32_t* list;     // continuation rounds: the slice's rays still going (nullptr: every ray)
-    uint32_t* cont_out;       // k_extend_curves<true>: the rays whose traversal goes on ...
-    uint32_t* cont_n;         // ... and their count
-    uint32_t K, S;
-    int32_t lds;              // k_curve_trav's stack entries per lane in LDS (<= RT_TRAV_LDS_STACK; tests lower it)
-    unsigned long long* segs; // the fused curve extend (FUSE): continuation segments counter
-    uint32_t depth;           // ... and the launch's path depth
-    uint32_t fin_batch;       // ... and its finish batch (finished lanes shaded and refilled together)
-};
-
-// Host side: the fused curve extend's launch (launch_extend): every depth from `depth` on in one launch
+// The fused curve extend's launch (launch_extend, k_extend_curves<FUSE>): every depth from `depth` on in
+// one launch; continuation segments are counted into *segs
 struct CurveFuse {
     unsigned long long* segs;
     uint32_t depth;
-};
-
-// Host side: a render lane's split-curve buffers (rt_api.cpp Lane::cs), handed to launch_extend.
-struct CurveSplit {
-    CurveWork w;              // per-ray arrays of `cap` rays (list / cont_out / cont_n are set per launch)
-    uint32_t* cont[2];        // continuation lists (ping-pong), cap entries each
-    uint32_t* cnt[2];         // their counts (device words)
-    uint32_t cap;             // rays per slice
 };
 
 // Per-render-chunk parameters shared by the kernels.

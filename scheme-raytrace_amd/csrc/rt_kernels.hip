@@ -1901,50 +1901,27 @@ __device__ __forceinline__ uint32_t wave_append(const int cls, const uint32_t sh
 // =====================================================================
 static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK <= 160 * 1024 / RT_CURVE_WAVES,
               "k_extend_curves: RT_CURVE_WAVES blocks of BezWave state and LDS stack columns must fit a CU's LDS");
-// the LIST kernel (no traversal stack) may run more waves per SIMD: its wave state without the
-// pending-sibling slots (RT_CURVE_LIST_SLOT 0) fits three 4-wave blocks per CU
-#ifndef RT_CURVE_LIST_WAVES
-#define RT_CURVE_LIST_WAVES 2
-#endif
-#ifndef RT_CURVE_LIST_SLOT
-#define RT_CURVE_LIST_SLOT RT_BEZ_SLOT
-#endif
-template <bool LIST> using CurveWave = BezWaveT<LIST ? (RT_CURVE_LIST_SLOT != 0) : (RT_BEZ_SLOT != 0)>;
-static_assert(4 * sizeof(CurveWave<true>) <= 160 * 1024 / RT_CURVE_LIST_WAVES,
-              "k_extend_curves<true>: RT_CURVE_LIST_WAVES blocks of wave state must fit a CU's LDS");
 #ifndef RT_CURVE_PREFETCH
 #define RT_CURVE_PREFETCH 1            // load the lane's next BVH4 node one iteration ahead (32 VGPRs)
 #endif
-// LIST (the split curve extend, round 5): the BVH4 walk runs ahead in k_curve_trav, which leaves each ray
-// of the slice a list of curve candidates (curve, box entry t) in traversal order and the closest hit of
-// everything else (the groups before the BVH, sphere leaves); this kernel walks the list instead of the
-// tree: a candidate whose box starts beyond the ray's closest hit so far is skipped — the test the tree
-// walk culls that box with — and the rest go through the same batches.  Its registers hold no traversal
-// state (no node, no stack, no box ray).  A ray whose traversal stopped at the list's capacity is handed
-// back (closest, best) and continues in the next round (cw.cont_out).  k: slice-local ray index (the ray
-// queue's k0 + k), claimed in order, or through cw.list in continuation rounds.
-// RTAMD_CURVE_DEBUG (diagnostics): [0] candidates listed, [1] candidates tested (not skipped), [2] BVH4 nodes
-// visited by k_curve_trav, [3] rays listed (summed over rounds)
-__device__ unsigned long long g_split_dbg[4];
-__device__ int g_split_dbg_on;
-// FUSE (1: device libm, 2: the exact libm; !LIST): every depth from cw.depth on in one launch.  A lane
+// FUSE (1: device libm, 2: the exact libm): every depth from fz.depth on in one launch.  A lane
 // whose ray is resolved shades it on the spot (shade_hit, the wavefront shade's own code: any material,
 // no Perlin tables, no light mixture — launch_extend checks the scene) and, if the path goes on, stores
 // the scattered ray in place (same slot) and walks it at once, so the launch drains once per chunk
 // instead of once per depth (C5: ~1.1 ms per depth launch, about a quarter of the curve kernel's time).
-// Paths that end write their sample; continuation segments are counted into *cw.segs.
+// Paths that end write their sample; continuation segments are counted into *fz.segs.
 template <bool EX>
 __device__ __forceinline__ bool fused_shade(const DevScene& sc, const RenderParams& rp, PathRegs& p, const double t,
                                             const int32_t leaf, v3& L);   // below shade_hit
-template <bool LIST, int FUSE = 0>
-__global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
+template <int FUSE = 0>
+__global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const DevScene sc, const RenderParams rp,
                                                        const PathState st, const QView in, uint32_t n, HitBuf hit,
                                                        uint32_t shard_cap, uint32_t* __restrict__ counts,
                                                        const bool depth0, unsigned int* __restrict__ claim,
-                                                       const CurveWork cw, const uint32_t k0) {
-    extern __shared__ uint32_t s_lstack[];          // per-lane BVH4 stack column, 256 x sc.lds4 (dynamic LDS; !LIST)
-    __shared__ CurveWave<LIST> s_bw[4];
-    CurveWave<LIST>& W = s_bw[threadIdx.x >> 6];
+                                                       const CurveFuse fz) {
+    extern __shared__ uint32_t s_lstack[];          // per-lane BVH4 stack column, 256 x sc.lds4 (dynamic LDS)
+    __shared__ BezWave s_bw[4];
+    BezWave& W = s_bw[threadIdx.x >> 6];
     uint32_t* lstk = s_lstack + threadIdx.x;
     const uint32_t stride = blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1952,15 +1929,9 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
     const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE], bz = sc.leaf_base[LEAF_BEZIER];
     int gb = 0;                                     // the world BVH group (commit_scene builds at most one)
     while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
-    static_assert(!(LIST && FUSE), "the fused curve extend walks the tree");
     bool active = false, exhausted = false, trav = false;
     uint32_t i = 0, queued = 0;
-    uint32_t dep = FUSE ? cw.depth : 0u, fsegs = 0;  // FUSE: the lane's path depth, continuation segments
-    // LIST: the lane's ray (slice-local), its list cursor and length, whether its traversal goes on in the
-    // next round, and the next candidate (loaded one iteration ahead)
-    uint32_t k = 0, cj = 0, nc = 0;
-    bool tmore = false;
-    uint2 nxt = make_uint2(0u, 0u);
+    uint32_t dep = FUSE ? fz.depth : 0u, fsegs = 0;  // FUSE: the lane's path depth, continuation segments
     // The ray itself (o, d, time) is not kept in registers across iterations: the BVH step needs only
     // its box-test form and t scale, the sphere leaves and the finish reload it (ray_of below), so stage
     // B's walk state fits beside the loop's (registers cap the waves per SIMD, RT_CURVE_WAVES)
@@ -1971,7 +1942,7 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
     int32_t bcls = -1;
     BoxRayW br{};                                   // rays from anywhere (BoxRayW)
 #if RT_CURVE_PREFETCH
-    BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead (!LIST)
+    BvhNode4 N{};                                   // the lane's next node, loaded one iteration ahead
 #endif
     auto ray_of = [&](v3& o, v3& d, double& tm) {
         const RayRec R = st.ray[i];
@@ -1994,7 +1965,7 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         --sp;
         return (int32_t)(sp < lds4 ? lstk[sp * stride] : sc.stk_ovf[(size_t)(sp - lds4) * sc.ovf_lanes + ovf_lane]);
     };
-    // a lane takes ray i (its closest hit from scratch): the groups before the BVH, then the BVH4 walk (!LIST)
+    // a lane takes ray i (its closest hit from scratch): the groups before the BVH, then the BVH4 walk
     auto start_ray = [&]() {
         v3 o, d;
         double tm;
@@ -2054,10 +2025,8 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         // round trips, which cost the wave the same whether one lane or sixteen take them.
         const bool fin = active && !trav && pb >= pe && W.done[lane] == queued;
         const unsigned long long fin_m = __ballot(fin);
-        const int fin_batch = FUSE ? (int)cw.fin_batch : RT_CURVE_FINISH_BATCH;   // FUSE: the batch shades too
-        const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= fin_batch ||
+        const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= RT_CURVE_FINISH_BATCH ||
                                              fin_m == __ballot(active));
-        bool cont = false;                                   // LIST: handed back to the next round
         if constexpr (FUSE != 0) {
             if (fin && flush) {                              // shade here; a scattered path goes on in this lane
                 PathRegs p;
@@ -2081,11 +2050,6 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
                     active = false;
                 }
             }
-        } else if (fin && flush && LIST && tmore) {
-            cw.closest[k] = closest;
-            cw.best[k] = best;
-            cont = true;
-            active = false;
         } else if (fin && flush) {
             if (gb + 1 < sc.n_groups || best < 0) {          // the groups after the BVH or the sky: the ray again
                 v3 o, d;
@@ -2118,16 +2082,6 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
                                                     counts, shard_cap);
             if (cls >= 0 && slot != kNoSlot) hit.h[(size_t)cls * hit.stride + slot] = hr;
         }
-        if constexpr (LIST) {                                // the continuation list: one atomic per wave
-            const unsigned long long cm = __ballot(cont);
-            if (cm) {
-                const int leader = __ffsll((long long)cm) - 1;
-                uint32_t base = 0;
-                if ((int)lane == leader) base = atomicAdd(cw.cont_n, (uint32_t)__popcll(cm));
-                base = (uint32_t)__shfl((int)base, leader, 64);
-                if (cont) cw.cont_out[base + lanes_below(cm)] = k;
-            }
-        }
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
 #endif
@@ -2143,26 +2097,9 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
             if (!active && !dead) {
                 const uint32_t kk = base + lanes_below(need);
                 if (kk < n) {
-                    if constexpr (LIST) {
-                        k = cw.list ? cw.list[kk] : kk;
-                        i = qphys(qm, k0 + k);
-                        v3 o, d;
-                        double tm;
-                        ray_of(o, d, tm);
-                        closest = cw.closest[k];             // k_curve_trav: groups before the BVH, sphere leaves
-                        best = cw.best[k];
-                        bcls = best >= 0 ? (int32_t)sc.leaf_cls[best] : -1;
-                        const uint32_t h = cw.ncand[k];
-                        nc = h & 0x7FFFFFFFu;
-                        tmore = (h >> 31) != 0u;
-                        cj = 0;
-                        tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));
-                        bez_ray(o, d, W.ray[lane]);
-                        trav = nc > 0u;
-                        if (trav) nxt = reinterpret_cast<const uint2*>(cw.cand)[(size_t)k * cw.K];
-                    } else {
+                    {
                         i = qphys(qm, kk);
-                        dep = FUSE ? cw.depth : 0u;
+                        dep = FUSE ? fz.depth : 0u;
                         start_ray();
                     }
                     W.done[lane] = 0u;
@@ -2179,18 +2116,7 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
 #endif
         // 3. one BVH4 step (bvh_closest_curves over the collapsed tree): the node's hit children
         //    nearest first, the nearest entered, the others pushed
-        if (LIST && active && trav && pb >= pe) {
-            // the next candidate of the list: queued unless its box starts beyond the closest hit so far
-            // (the tree walk's cull of that box: its entry t against f32_up(closest * tscale))
-            const uint2 c = nxt;
-            ++cj;
-            trav = cj < nc;
-            if (trav) nxt = reinterpret_cast<const uint2*>(cw.cand)[(size_t)k * cw.K + cj];
-            if (!(__uint_as_float(c.y) > f32_up(closest * tscale))) {
-                pb = (int)c.x; pe = pb + 1;
-                if (g_split_dbg_on) atomicAdd(&g_split_dbg[1], 1ull);
-            }
-        } else if (!LIST && active && trav && pb >= pe) {
+        if (active && trav && pb >= pe) {
             if (node >= 0) {
 #if !RT_CURVE_PREFETCH
                 const BvhNode4 N = sc.bvh4[node];
@@ -2272,7 +2198,7 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         }
 #if RT_CURVE_PREFETCH
         // the next node's record, in flight while the batches below run (+5 % at C5 with 2 waves per SIMD)
-        if (!LIST && active && trav && node >= 0) N = sc.bvh4[node];
+        if (active && trav && node >= 0) N = sc.bvh4[node];
 #endif
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk3 += t - st_t; st_t = t; }
@@ -2328,7 +2254,7 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
     }
     if constexpr (FUSE != 0) {                       // continuation segments: wave sum, one atomic per wave
         for (int off = 32; off > 0; off >>= 1) fsegs += __shfl_xor(fsegs, off, 64);
-        if (lane == 0u && fsegs) atomicAdd(cw.segs, (unsigned long long)fsegs);
+        if (lane == 0u && fsegs) atomicAdd(fz.segs, (unsigned long long)fsegs);
     }
 #ifdef RT_STATS
     RT_STAT(20, st_steps); RT_STAT(21, st_busy); RT_STAT(22, st_wait);
@@ -2338,158 +2264,6 @@ __global__ __launch_bounds__(256, LIST ? RT_CURVE_LIST_WAVES : RT_CURVE_WAVES) v
         RT_STAT(42, st_clk1); RT_STAT(43, st_clk2); RT_STAT(44, st_clk3);   // kernel / stage A clocks per wave
     }
 #endif
-}
-
-// =====================================================================
-// k_curve_trav — the split curve extend's traversal (LIST mode of k_extend_curves tests what it lists):
-// one thread per ray of the slice walks the curve tree's BVH4 as k_extend_curves' own walk does (the same
-// slab test, the hit children nearest first) and, instead of queueing the curves it reaches, lists them
-// with their box's entry t; spheres in the tree are tested on the spot, and the groups before the BVH
-// are taken first (hit-obj-list order, geometry.scm:33-50).  Without the curve tests the thread holds
-// ~70 registers instead of ~230, so many more waves hide the dependent node fetches of a 64-MB tree.  A
-// list holds K candidates: a walk that would pass K stops before the node or leaf and saves its next node
-// and stack (cw.save); RESUME rounds restore them, with the closest hit the curve tests have found since,
-// which also prunes the rest of the walk.
-// =====================================================================
-#ifndef RT_TRAV_WAVES
-#define RT_TRAV_WAVES 6                // waves per SIMD k_curve_trav is compiled for
-#endif
-#ifndef RT_TRAV_LDS_STACK
-#define RT_TRAV_LDS_STACK 24           // stack entries per lane in LDS (the rest in the ray's save area)
-#endif
-static_assert(RT_TRAV_LDS_STACK * 256 * 4 * RT_TRAV_WAVES <= 160 * 1024, "k_curve_trav: the LDS stack columns fit a CU");
-template <bool RESUME>
-__global__ __launch_bounds__(256, RT_TRAV_WAVES) void k_curve_trav(const DevScene sc, const PathState st, const QView in,
-                                                                   const uint32_t k0, const uint32_t n, const CurveWork cw,
-                                                                   const bool depth0) {
-    __shared__ uint32_t s_stk[RT_TRAV_LDS_STACK * 256];
-    const int LDS = cw.lds;                           // <= RT_TRAV_LDS_STACK (rt_api.cpp ensure_curve_split)
-    constexpr int32_t kNone = INT32_MIN;
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t k = RESUME ? cw.list[t] : t;
-    const uint32_t i = qphys(qmap(in), k0 + k);
-    const RayRec R = st.ray[i];
-    const v3 o = mk(R.ox, R.oy, R.oz), d = mk(R.dx, R.dy, R.dz);
-    const double tm = depth0 ? st.tm[i] : 0.0;
-    uint32_t* lstk = s_stk + threadIdx.x;
-    int32_t* sv = cw.save + (size_t)k * cw.S;         // [0] next node, [1] stack depth, [2 + e] entry e
-    const int scap = (int)cw.S - 2;                   // >= commit_scene's bound on the walk's stack (stack4)
-    double closest;
-    int32_t best, node;
-    int sp;
-    if constexpr (!RESUME) {
-        int gb = 0;                                   // the world BVH group (commit_scene builds at most one)
-        while (gb < sc.n_groups && sc.groups[gb].type != GROUP_BVH) ++gb;
-        closest = kTmax;
-        best = -1;
-        for (int g = 0; g < gb; ++g) group_closest<0>(sc, sc.groups[g], o, d, tm, closest, best, nullptr);
-        node = gb < sc.n_groups ? sc.bvh4_root : kNone;
-        sp = 0;
-    } else {
-        closest = cw.closest[k];
-        best = cw.best[k];
-        node = sv[0];
-        sp = sv[1];
-        for (int e = 0; e < min(sp, LDS); ++e) lstk[e * 256] = (uint32_t)sv[2 + e];
-    }
-    const BoxRayW br = box_ray_w(o, d);               // rays from anywhere (BoxRayW)
-    const double tscale = fmax(1.0, 1.0 / sqrt(dot(d, d)));   // a curve's z is along unit(d) (Q10)
-    const uint32_t K = cw.K;
-    CurveCand* out = cw.cand + (size_t)k * K;
-    uint32_t nc = 0;
-    auto push = [&](const int32_t e) {
-        if (sp >= scap) { raise_fault(RT_FAULT_PATH); return; }
-        if (sp < LDS) lstk[sp * 256] = (uint32_t)e;
-        else sv[2 + sp] = e;
-        ++sp;
-    };
-    auto pop = [&]() -> int32_t {
-        if (sp == 0) return kNone;
-        --sp;
-        return sp < LDS ? (int32_t)lstk[sp * 256] : sv[2 + sp];
-    };
-    const int32_t bs = sc.leaf_base[LEAF_SPHERE], bm = sc.leaf_base[LEAF_MSPHERE];
-    // every node and leaf is visited at most once per ray (over all rounds)
-    const uint32_t cap = 2u * (uint32_t)(sc.n_bvh4 + sc.n_bleaf) + 16u;
-    uint32_t dbg_nodes = 0;
-    for (uint32_t it = 0; node != kNone; ++it) {
-        if (it > cap) { raise_fault(RT_FAULT_PATH); node = kNone; break; }
-        if (node >= 0) {
-            if (nc + 4u > K) break;                   // a node lists up to 4 curves: the next round takes it
-            ++dbg_nodes;
-            const BvhNode4 N = sc.bvh4[node];
-            const float tcap = f32_up(closest * tscale);
-            float key[4];
-            int32_t ref[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float tx0 = fmaf(N.lo[0][j], br.ix, -br.lx), tx1 = fmaf(N.hi[0][j], br.ix, -br.hx);
-                const float ty0 = fmaf(N.lo[1][j], br.iy, -br.ly), ty1 = fmaf(N.hi[1][j], br.iy, -br.hy);
-                const float tz0 = fmaf(N.lo[2][j], br.iz, -br.lz), tz1 = fmaf(N.hi[2][j], br.iz, -br.hz);
-                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tcap));
-                key[j] = (tn <= tf && j < N.n) ? tn : INFINITY;   // slab ends are finite: INFINITY = missed
-                ref[j] = N.ref[j];
-            }
-            auto cswap = [&](const int x, const int y) {
-                const bool sw = key[y] < key[x];
-                const float kx = key[x];
-                const int32_t rx = ref[x];
-                key[x] = sw ? key[y] : kx; key[y] = sw ? kx : key[y];
-                ref[x] = sw ? ref[y] : rx; ref[y] = sw ? rx : ref[y];
-            };
-            cswap(0, 1); cswap(2, 3); cswap(0, 2); cswap(1, 3); cswap(1, 2);
-            // the hit children nearest first: single-curve leaves listed with their entry t, then the
-            // nearest other child entered and the rest pushed (farthest first, so the nearer pop first)
-            int32_t enter = kNone;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (key[j] != INFINITY && ~ref[j] >= kDirectCurve)
-                    out[nc++] = CurveCand{(uint32_t)(~ref[j] - kDirectCurve), __float_as_uint(key[j])};
-#pragma unroll
-            for (int j = 3; j >= 0; --j)
-                if (key[j] != INFINITY && !(~ref[j] >= kDirectCurve)) {
-                    if (enter != kNone) push(enter);
-                    enter = ref[j];
-                }
-            node = enter != kNone ? enter : pop();
-        } else if (~node >= kDirectCurve) {           // the root itself a single-curve leaf
-            out[nc++] = CurveCand{(uint32_t)(~node - kDirectCurve), 0u};
-            node = pop();
-        } else {
-            const BvhLeaf L = sc.bleaf[~node];
-            if (nc > 0u && nc + (uint32_t)L.bn > K) break;   // its curves in the next round's list
-            if (L.sn + L.mn > 0) {
-                const double a = dot(d, d), ia = 1.0 / a;
-                for (int s = L.sb; s < L.sb + L.sn; ++s) {
-                    const SphereRec S = sc.sph[s];
-                    sphere_test(o, d, a, ia, mk(S.cx, S.cy, S.cz), S.rr, bs + s, closest, best);
-                }
-                for (int s = L.mb; s < L.mb + L.mn; ++s) {
-                    const MSphereRec S = sc.msph[s];
-                    const double frac = (tm - S.t0) / S.den;
-                    const v3 cen = mk(S.c0x, S.c0y, S.c0z) + mk(S.dcx, S.dcy, S.dcz) * frac;
-                    sphere_test(o, d, a, ia, cen, S.rr, bm + s, closest, best);
-                }
-            }
-            for (int b = L.bb; b < L.bb + L.bn && nc < K; ++b) out[nc++] = CurveCand{(uint32_t)b, 0u};   // tn 0: tested
-            node = pop();
-        }
-    }
-    cw.closest[k] = closest;
-    cw.best[k] = best;
-    cw.ncand[k] = nc | (node != kNone ? 0x80000000u : 0u);
-    if (g_split_dbg_on) {
-        atomicAdd(&g_split_dbg[0], (unsigned long long)nc);
-        atomicAdd(&g_split_dbg[2], (unsigned long long)dbg_nodes);
-        atomicAdd(&g_split_dbg[3], 1ull);
-    }
-    if (node != kNone) {
-        sv[0] = node;
-        sv[1] = sp;
-        for (int e = 0; e < min(sp, LDS); ++e) sv[2 + e] = (int32_t)lstk[e * 256];
-    }
 }
 
 #ifndef RT_EXTLDS_BLOCK
@@ -3255,28 +3029,16 @@ static uint32_t curve_blocks() {            // cap on the persistent curve grid 
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u << 20;
 }
 bool curve_persistent() { return curve_blocks() > 0u; }   // the host's check before a fused launch
-static bool curve_debug() {                 // RTAMD_CURVE_DEBUG=1: the split extend's rounds on stderr (diagnostics)
-    const char* e = std::getenv("RTAMD_CURVE_DEBUG");
-    return e != nullptr && e[0] == '1';
-}
-#ifndef RT_CURVE_SPLIT_DEFAULT
-#define RT_CURVE_SPLIT_DEFAULT 0       // the split curve extend by default (RTAMD_CURVE_SPLIT=0 / 1 overrides)
-#endif
-bool curve_split() {                        // RTAMD_CURVE_SPLIT=1 / 0: the split / one-kernel curve extend
-    const char* e = std::getenv("RTAMD_CURVE_SPLIT");   // read per launch: tests switch it inside one process
-    return e != nullptr && e[0] != '\0' ? e[0] != '0' : RT_CURVE_SPLIT_DEFAULT != 0;
-}
 // resident blocks of a curve kernel instance for its dynamic LDS, cached per (kernel, device, LDS bytes)
 static hipError_t curve_occupancy(const void* f, const size_t lds, uint32_t* out) {
-    static const void* occ_f[4] = {nullptr, nullptr, nullptr, nullptr};
-    static int occ_dev[4] = {-1, -1, -1, -1};
-    static size_t occ_lds[4] = {~(size_t)0, ~(size_t)0, ~(size_t)0, ~(size_t)0};
-    static uint32_t occ_blocks[4] = {0, 0, 0, 0};
+    static const void* occ_f[3] = {nullptr, nullptr, nullptr};
+    static int occ_dev[3] = {-1, -1, -1};
+    static size_t occ_lds[3] = {~(size_t)0, ~(size_t)0, ~(size_t)0};
+    static uint32_t occ_blocks[3] = {0, 0, 0};
     int dev = 0;
     HIP_RETURN_IF(hipGetDevice(&dev));
-    const int slot = f == reinterpret_cast<const void*>(&k_extend_curves<true>) ? 1
-                   : f == reinterpret_cast<const void*>(&k_extend_curves<false, 1>) ? 2
-                   : f == reinterpret_cast<const void*>(&k_extend_curves<false, 2>) ? 3 : 0;
+    const int slot = f == reinterpret_cast<const void*>(&k_extend_curves<1>) ? 1
+                   : f == reinterpret_cast<const void*>(&k_extend_curves<2>) ? 2 : 0;
     if (occ_f[slot] != f || occ_lds[slot] != lds || occ_dev[slot] != dev) {
         int per_cu = 0, cus = 0;
         HIP_RETURN_IF(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, lds));
@@ -3289,79 +3051,21 @@ static hipError_t curve_occupancy(const void* f, const size_t lds, uint32_t* out
     *out = occ_blocks[slot];
     return hipSuccess;
 }
-// The split curve extend over n rays: slices of cs->cap rays; per slice k_curve_trav lists every ray's
-// candidates and k_extend_curves<true> tests them, then rounds for the rays whose lists were full (their
-// count read back on the host: the rounds shrink fast, and curve scenes run one render lane)
-static hipError_t launch_curves_split(const DevScene& sc, const RenderParams& rp, const PathState& st, const QView& in,
-                                      uint32_t n, const HitBuf& hit, uint32_t shard_cap, uint32_t* counts, bool depth0,
-                                      unsigned int* claim, const CurveSplit& cs, hipStream_t s) {
-    uint32_t occ = 0;
-    HIP_RETURN_IF(curve_occupancy(reinterpret_cast<const void*>(&k_extend_curves<true>), 0, &occ));
-    const int dbg = curve_debug() ? 1 : 0;
-    HIP_RETURN_IF(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_split_dbg_on), &dbg, sizeof dbg, 0, hipMemcpyHostToDevice, s));
-    if (occ > curve_blocks()) occ = curve_blocks();
-    if (occ > sc.ring_waves / 4u) occ = sc.ring_waves / 4u;       // one survivor ring per wave
-    if (occ == 0u) occ = 1u;
-    for (uint32_t k0 = 0; k0 < n; k0 += cs.cap) {
-        const uint32_t ns = n - k0 < cs.cap ? n - k0 : cs.cap;
-        CurveWork w = cs.w;
-        w.list = nullptr;
-        int cur = 0;
-        uint32_t m = ns;                                          // rays of this round
-        for (int round = 0; m > 0u; ++round) {
-            w.cont_out = cs.cont[cur];
-            w.cont_n = cs.cnt[cur];
-            HIP_RETURN_IF(hipMemsetAsync(cs.cnt[cur], 0, sizeof(uint32_t), s));
-            HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-            const uint32_t tb = (m + 255u) / 256u;
-            if (round == 0)
-                hipLaunchKernelGGL(k_curve_trav<false>, dim3(tb), dim3(256), 0, s, sc, st, in, k0, m, w, depth0);
-            else
-                hipLaunchKernelGGL(k_curve_trav<true>, dim3(tb), dim3(256), 0, s, sc, st, in, k0, m, w, depth0);
-            HIP_RETURN_IF(hipGetLastError());
-            const uint32_t pb = tb < occ ? tb : occ;
-            hipLaunchKernelGGL(k_extend_curves<true>, dim3(pb), dim3(256), 0, s, sc, rp, st, in, m, hit, shard_cap,
-                               counts, depth0, claim, w, k0);
-            HIP_RETURN_IF(hipGetLastError());
-            uint32_t next = 0;
-            HIP_RETURN_IF(hipMemcpyAsync(&next, cs.cnt[cur], sizeof next, hipMemcpyDeviceToHost, s));
-            HIP_RETURN_IF(hipStreamSynchronize(s));
-            if (next > m) return hipErrorIllegalState;            // a list can only shrink
-            if (curve_debug()) std::fprintf(stderr, "curve split: slice %u+%u round %d rays %u -> %u\n", k0, ns, round, m, next);
-            w.list = cs.cont[cur];
-            cur ^= 1;
-            m = next;
-        }
-    }
-    if (dbg) {
-        unsigned long long v[4] = {0, 0, 0, 0};
-        HIP_RETURN_IF(hipStreamSynchronize(s));
-        HIP_RETURN_IF(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_split_dbg), sizeof v));
-        std::fprintf(stderr, "curve split: n %u listed %llu tested %llu nodes %llu ray-rounds %llu (per ray %.2f %.2f %.2f %.3f)\n",
-                     n, v[0], v[1], v[2], v[3], (double)v[0] / n, (double)v[1] / n, (double)v[2] / n, (double)v[3] / n);
-        const unsigned long long z[4] = {0, 0, 0, 0};
-        HIP_RETURN_IF(hipMemcpyToSymbol(HIP_SYMBOL(g_split_dbg), z, sizeof z));
-    }
-    return hipSuccess;
-}
 hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams& rp, const PathState& st, const QView& in,
                          uint32_t n, const HitBuf& hit, uint32_t shard_cap,
-                         uint32_t* counts, bool depth0, unsigned int* claim, const CurveSplit* cs,
-                         const CurveFuse* fuse, hipStream_t s) {
+                         uint32_t* counts, bool depth0, unsigned int* claim, const CurveFuse* fuse, hipStream_t s) {
     const uint32_t blocks = (n + 255u) / 256u;
     const size_t lds = (size_t)256 * (size_t)(sc.lane_stack > 0 ? sc.lane_stack : 1) * sizeof(uint32_t);
     // the persistent curve kernel: every curve in the world BVH (its groups outside the BVH are spheres and
     // rects only: group_closest<0>, so the per-lane curve walk is not compiled into it)
     if (scene_features(sc) == kFeatCurves && sc.bvh_has_bez && sc.bez_groups == 0 && claim && curve_blocks() > 0) {
-        if (cs && cs->cap > 0u && curve_split())
-            return launch_curves_split(sc, rp, st, in, n, hit, shard_cap, counts, depth0, claim, *cs, s);
         // resident blocks only: later blocks would find the rays claimed.  The BVH4 walk's LDS stack column
         // holds lds4 entries per lane (the rest in the overflow area).  Occupancy per (device, LDS bytes)
         const size_t clds = (size_t)256 * (size_t)(sc.lds4 > 0 ? sc.lds4 : 1) * sizeof(uint32_t);
         uint32_t occ_blocks = 0;
-        const void* kf = !fuse ? reinterpret_cast<const void*>(&k_extend_curves<false, 0>)
-                       : rp.exact_libm ? reinterpret_cast<const void*>(&k_extend_curves<false, 2>)
-                                       : reinterpret_cast<const void*>(&k_extend_curves<false, 1>);
+        const void* kf = !fuse ? reinterpret_cast<const void*>(&k_extend_curves<0>)
+                       : rp.exact_libm ? reinterpret_cast<const void*>(&k_extend_curves<2>)
+                                       : reinterpret_cast<const void*>(&k_extend_curves<1>);
         HIP_RETURN_IF(curve_occupancy(kf, clds, &occ_blocks));
         uint32_t pb = blocks < occ_blocks ? blocks : occ_blocks;
         if (pb > curve_blocks()) pb = curve_blocks();
@@ -3370,23 +3074,15 @@ hipError_t launch_extend(const DevScene& sc, const DevScene*, const RenderParams
         if (pb > sc.ring_waves / 4u) pb = sc.ring_waves / 4u;   // one survivor ring per wave
         if (pb == 0u) pb = 1u;
         HIP_RETURN_IF(hipMemsetAsync(claim, 0, sizeof(unsigned int), s));
-        CurveWork w{};
         if (!fuse) {
-            hipLaunchKernelGGL((k_extend_curves<false, 0>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
-                               shard_cap, counts, depth0, claim, w, 0u);
+            hipLaunchKernelGGL((k_extend_curves<0>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                               shard_cap, counts, depth0, claim, CurveFuse{});
+        } else if (rp.exact_libm) {
+            hipLaunchKernelGGL((k_extend_curves<2>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                               shard_cap, counts, false, claim, *fuse);
         } else {
-            w.segs = fuse->segs;
-            w.depth = fuse->depth;
-            {
-                static const int fb = std::getenv("RTAMD_FUSE_BATCH") ? std::atoi(std::getenv("RTAMD_FUSE_BATCH")) : 0;
-                w.fin_batch = fb > 0 ? (uint32_t)fb : (uint32_t)RT_CURVE_FINISH_BATCH;
-            }
-            if (rp.exact_libm)
-                hipLaunchKernelGGL((k_extend_curves<false, 2>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
-                                   shard_cap, counts, false, claim, w, 0u);
-            else
-                hipLaunchKernelGGL((k_extend_curves<false, 1>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
-                                   shard_cap, counts, false, claim, w, 0u);
+            hipLaunchKernelGGL((k_extend_curves<1>), dim3(pb), dim3(256), clds, s, sc, rp, st, in, n, hit,
+                               shard_cap, counts, false, claim, *fuse);
         }
         return hipGetLastError();
     }

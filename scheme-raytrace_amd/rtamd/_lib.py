@@ -130,6 +130,10 @@ _SIGNATURES = {
     "rt_comm_create": [ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int, _c_int_p],
     "rt_comm_destroy": [ctypes.c_int],
     "rt_gather_shards": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+    "rt_gather_layout": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                         ctypes.POINTER(ctypes.c_int64)],
+    "rt_gather_shards_local": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_void_p],
 }
 
 #: every symbol include/rt.h declares (tests check the .so exports all of them)

@@ -3,7 +3,8 @@
 trace-all has no cross-pixel dependence (main.scm:471-491) and the counter RNG
 keys every sample by (seed, pixel, sample), so a frame splits into disjoint
 pixel sets with no exchange until the end.  Rank r renders the interleaved
-16x16 tiles (tx, ty) with (tx + 3 ty) % world == r (rt_shard_pixels) into a COMPACT accumulator
+16x16 tiles (tx, ty) with (tx + k ty) % world == r (k the smallest odd prime not dividing world;
+rt_shard_pixels) into a COMPACT accumulator
 — its own pixels only, in shard order (rt_render_shard_device) — and rank 0
 gathers the shards over the process group (RCCL over xGMI with the "nccl"
 backend; gloo on the CPU) and scatters them into the y-up frame.  Each rank

@@ -354,3 +354,23 @@ def shard_pixels(nx, ny, shard, nshard):
     call("rt_shard_pixels", nx, ny, shard, nshard, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
          ctypes.byref(n))
     return out
+
+
+def gather_layout(nx, ny, world):
+    """rt_gather_layout (host only): per rank its shard's pixel count and the offset of its pixels in the
+    ranks' concatenated pixel lists; rank 0 receives rank r's compact accumulator at doubles
+    3 * (offset[r] - count[0]) of its receive buffer."""
+    cnt = np.zeros(world, dtype=np.int64)
+    off = np.zeros(world, dtype=np.int64)
+    call("rt_gather_layout", nx, ny, world, cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+         off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    return cnt, off
+
+
+def gather_shards_local(nx, ny, shard_ptrs, frame_ptr, ctx=None, stream=None):
+    """rt_gather_shards_local: every shard's compact accumulator (device pointers, shard r in entry r) on
+    this context's device into the frame — rt_gather_shards' receive layout and placement without RCCL."""
+    ctx = ctx or default_context()
+    arr = (ctypes.c_void_p * len(shard_ptrs))(*[ctypes.c_void_p(p) for p in shard_ptrs])
+    call("rt_gather_shards_local", ctx.handle, nx, ny, len(shard_ptrs), arr, ctypes.c_void_p(frame_ptr),
+         ctypes.c_void_p(stream or 0))

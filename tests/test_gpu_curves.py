@@ -237,13 +237,12 @@ def test_few_curves_among_spheres_large_launch(sched, oracle_mod, monkeypatch):
 
 
 def test_curve_walk_stack_overflow_bitwise(sched, monkeypatch):
-    """The curve walks push up to three children per node; commit_scene bounds
-    their stack (rt_scene_info.curve_stack), and entries past the LDS column go
-    to HBM: k_curve_trav's per-ray save area (which also carries a continuing
-    walk into the next round), the one-kernel extend's per-lane overflow area
-    (one region per render lane).  With the LDS column cut to one entry (RTAMD_CURVE_LDS_STACK=1) every
-    deeper push takes that path, on two render lanes: the image must not
-    change by a bit."""
+    """The curve walk pushes up to three children per node; commit_scene bounds
+    its stack (rt_scene_info.curve_stack), and entries past the LDS column go
+    to the per-lane overflow area in HBM (one region per render lane).  With
+    the LDS column cut to one entry (RTAMD_CURVE_LDS_STACK=1) every deeper push
+    takes that path, on two render lanes, fused over the depths and one launch
+    per depth: the image must not change by a bit."""
     nx, ny, spp = 96, 64, 4
     _opts(sched, tail_off=1, lanes=2, max_paths=nx * ny)
     base = np.zeros(nx * ny * 3)
@@ -255,16 +254,11 @@ def test_curve_walk_stack_overflow_bitwise(sched, monkeypatch):
     gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, low)
     print("curve walk stack: bound %d, LDS entries 1 vs %d" % (info["curve_stack"], info["tree_depth"]))
     assert np.array_equal(base, low)
-    # the same for the one-kernel curve extend (its walk's overflow area) and for the split extend with short
-    # lists (k_curve_trav's save area across continuation rounds)
-    for env in ({"RTAMD_CURVE_SPLIT": "0"}, {"RTAMD_CURVE_SPLIT": "1"}, {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_K": "6"}):
-        for kk, vv in env.items():
-            monkeypatch.setenv(kk, vv)
-        other = np.zeros_like(base)
-        gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, other)
-        assert np.array_equal(base, other), env
-        for kk in env:
-            monkeypatch.delenv(kk)
+    # the same with one curve-kernel launch per depth
+    monkeypatch.setenv("RTAMD_CURVE_FUSE", "0")
+    other = np.zeros_like(base)
+    gpu.render_host(scenes.cornell_curves(nx, ny, n_curves=1 << 14), nx, ny, 0, spp, SEED, other)
+    assert np.array_equal(base, other)
 
 
 def test_curve_ray_cap_faults_without_hang(sched, monkeypatch):

@@ -173,3 +173,46 @@ def test_bench_two_ranks_self_verifying(tmp_path):
     assert d["parity"]["pass"] and d["parity_frame"]["pass"]
     assert d["parity_frame"]["pixels_gt_1e-9"] <= max(2, d["parity_frame"]["pixels"] // 200)
     assert d["per_rank_ms_per_step"]["render_max"] >= d["per_rank_ms_per_step"]["render_min"] > 0
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_gather_shards_local_world_n_equals_render_device(sched, world):
+    """rt_gather_shards' N > 1 receive layout and placement, executed on one GPU (round 6; RCCL cannot put
+    two ranks on one device): every shard of `world` rendered into its own compact accumulator
+    (rt_render_shard_device), then rt_gather_shards_local — the shared gather plan (rt_gather_layout's
+    counts / offsets, rank 0's receive buffer at 3 * (off[r] - count[0])) and placement kernel, with device
+    copies standing in for ncclRecv — must give rt_render_device's frame bit for bit, at world 3 (tile
+    stride 5) and 8, on a frame whose edge tiles are partial."""
+    import torch
+    from rtamd import gpu, scenes
+    nx, ny, spp = 200, 120, 3
+    scene = scenes.random_scene(nx, ny)
+    cnt, off = gpu.gather_layout(nx, ny, world)
+    shards = [torch.zeros(3 * int(c), dtype=torch.float64, device="cuda") for c in cnt]
+    frame = torch.full((nx * ny * 3,), -1.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()                             # torch's fills before the library's stream
+    for r, buf in enumerate(shards):
+        gpu.render_shard_device(scene, nx, ny, 0, spp, SEED, r, world, buf.data_ptr())
+    gpu.gather_shards_local(nx, ny, [b.data_ptr() for b in shards], frame.data_ptr())
+    full = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    gpu.render_device(scene, nx, ny, 0, spp, SEED, full.data_ptr())
+    torch.cuda.synchronize()
+    got, want = frame.cpu().numpy(), full.cpu().numpy()
+    assert (got >= 0).all()                              # every pixel was placed
+    assert np.array_equal(got, want)
+    # a second frame size on the same context rebuilds the plan
+    nx2, ny2 = 64, 40
+    sc2 = scenes.random_scene(nx2, ny2)
+    cnt2, _ = gpu.gather_layout(nx2, ny2, world)
+    sh2 = [torch.zeros(3 * int(c), dtype=torch.float64, device="cuda") for c in cnt2]
+    torch.cuda.synchronize()
+    for r, b in enumerate(sh2):
+        gpu.render_shard_device(sc2, nx2, ny2, 0, 1, SEED, r, world, b.data_ptr())
+    f2 = torch.zeros(nx2 * ny2 * 3, dtype=torch.float64, device="cuda")
+    w2 = torch.zeros_like(f2)
+    torch.cuda.synchronize()
+    gpu.gather_shards_local(nx2, ny2, [b.data_ptr() for b in sh2], f2.data_ptr())
+    gpu.render_device(sc2, nx2, ny2, 0, 1, SEED, w2.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(f2.cpu().numpy(), w2.cpu().numpy())

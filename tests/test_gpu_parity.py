@@ -511,10 +511,9 @@ def test_fused_curve_extend_bitwise(sched, monkeypatch, libm):
 @pytest.mark.parametrize("flat_curves", [False, True])
 def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     """Curves, spheres and moving spheres in one world BVH between rect
-    groups, through the wavefront: the split curve extend (traversal lists +
-    persistent curve tests, also over many continuation rounds), the one-kernel
-    persistent curve extend, the per-ray curve kernel and the flat list give
-    the same image bit for bit.
+    groups, through the wavefront: the persistent curve extend (fused over the
+    depths, and one launch per depth), the per-ray curve kernel and the flat
+    list give the same image bit for bit.
     flat_curves adds short, nearly straight curves whose subdivision depth
     ceil(log4(...)) is negative (bezier.scm:180-193: the root is a leaf); the
     flat list's per-lane test and the batched stage A/B must agree on them.
@@ -553,15 +552,12 @@ def test_curve_kernels_bitwise(sched, monkeypatch, flat_curves):
     sc = g.make_scene(objs, scenes.cornell_camera_for(nx, ny), g.sky_color)
     sched.set_option("tail_off", 1)
     imgs = []
-    # the flat list, the per-ray kernel, the split curve extend (k_curve_trav + k_extend_curves<true>; with
-    # 3 blocks; with 5-candidate lists, so rays continue over many rounds), the one-kernel persistent curve
-    # extend fused over the depths (the default: hits shaded in the kernel, every material of the scene;
-    # also with 3 blocks), and one launch per depth (RTAMD_CURVE_FUSE=0, also with 3 blocks)
-    for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {"RTAMD_CURVE_SPLIT": "1"},
-                {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_BLOCKS": "3"}, {"RTAMD_CURVE_SPLIT": "1", "RTAMD_CURVE_K": "5"},
-                {"RTAMD_CURVE_SPLIT": "0"}, {"RTAMD_CURVE_BLOCKS": "3"}, {"RTAMD_CURVE_FUSE": "0"},
-                {"RTAMD_CURVE_FUSE": "0", "RTAMD_CURVE_BLOCKS": "3"}):
-        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_K", "RTAMD_CURVE_SPLIT", "RTAMD_CURVE_FUSE"):
+    # the flat list, the per-ray kernel, the persistent curve extend fused over the depths (the default: hits
+    # shaded in the kernel, every material of the scene; also with 3 blocks), and one launch per depth
+    # (RTAMD_CURVE_FUSE=0, also with 3 blocks)
+    for env in ({"RTAMD_BVH_MIN": "1000000000"}, {"RTAMD_CURVE_BLOCKS": "0"}, {}, {"RTAMD_CURVE_BLOCKS": "3"},
+                {"RTAMD_CURVE_FUSE": "0"}, {"RTAMD_CURVE_FUSE": "0", "RTAMD_CURVE_BLOCKS": "3"}):
+        for k in ("RTAMD_BVH_MIN", "RTAMD_CURVE_BLOCKS", "RTAMD_CURVE_FUSE"):
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)

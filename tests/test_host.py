@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_errors_without_gpu():
     L = _lib.lib()
-    assert L.rt_abi_version() == 6
+    assert L.rt_abi_version() == 7
     h = ctypes.c_int(0)
     assert L.rt_scene_begin(424242, ctypes.byref(h)) != 0
     assert b"invalid context" in L.rt_last_error()
@@ -143,18 +143,68 @@ def test_constructor_type_checks():
         g.make_scene([], None, lambda r: None)
 
 
-@pytest.mark.parametrize("nx,ny,n", [(1920, 1080, 8), (33, 17, 3), (16, 16, 2), (5, 3, 4)])
+def _tile_stride(n):
+    return next(k for k in (3, 5, 7, 11, 13) if n % k)
+
+
+@pytest.mark.parametrize("nx,ny,n", [(1920, 1080, 8), (33, 17, 3), (16, 16, 2), (5, 3, 4), (1024, 1024, 6),
+                                     (1920, 1080, 3), (400, 300, 15)])
 def test_shard_partition_is_exact(nx, ny, n):
     from rtamd import gpu
     parts = [gpu.shard_pixels(nx, ny, r, n) for r in range(n)]
     allpix = np.concatenate(parts)
     assert allpix.size == nx * ny
     assert np.array_equal(np.sort(allpix), np.arange(nx * ny, dtype=np.uint32))
-    # tile (tx, ty) -> shard (tx + 3 ty) % n (16x16 tiles, row-major)
-    tx = (nx + 15) // 16
+    # tile (tx, ty) -> shard (tx + k ty) % n, k the smallest odd prime not dividing n (16x16 tiles, row-major)
+    k = _tile_stride(n)
     for r, p in enumerate(parts):
         x, y = p % nx, p // nx
-        assert np.all((3 * (y // 16) + x // 16) % n == r)
+        assert np.all((k * (y // 16) + x // 16) % n == r)
+    # round-6 advice: with a stride coprime to n every shard gets tiles of every column residue (the stride 3
+    # at n = 3 gave shard r the columns tx = r mod 3 only, whole-column stripes again)
+    tx, ty = (nx + 15) // 16, (ny + 15) // 16
+    if ty >= n and tx >= n:
+        for r, p in enumerate(parts):
+            cols = np.unique((p % nx) // 16)
+            assert cols.size == tx, (r, cols.size, tx)
+
+
+@pytest.mark.parametrize("nx,ny", [(1920, 1080), (1024, 1024), (200, 120), (33, 17)])
+def test_gather_layout_counts_and_offsets(nx, ny):
+    """rt_gather_layout — the receive layout rt_gather_shards (RCCL) and rt_gather_shards_local share — for
+    N = 2..8 at the C2 / C5 (1920x1080) and C4 (1024x1024) frame sizes: per rank the shard's pixel count
+    (= rt_shard_pixels'), offsets the prefix sums, rank 0's receive buffer holding ranks 1..N-1 back to back
+    at 3 (off[r] - count[0]) doubles, and the concatenated lists a permutation of the frame's pixels."""
+    from rtamd import gpu
+    for n in range(1, 9):
+        cnt, off = gpu.gather_layout(nx, ny, n)
+        want = np.array([gpu.shard_pixels(nx, ny, r, n).size for r in range(n)])
+        assert np.array_equal(cnt, want), (n, cnt, want)
+        assert off[0] == 0 and np.array_equal(off[1:], np.cumsum(cnt)[:-1])
+        assert cnt.sum() == nx * ny
+        recv = 3 * (off - cnt[0])                       # doubles, where rank r's shard lands on rank 0
+        assert recv[1] == 0 if n > 1 else True
+        for r in range(1, n - 1):
+            assert recv[r] + 3 * cnt[r] == recv[r + 1]
+        cat = np.concatenate([gpu.shard_pixels(nx, ny, r, n) for r in range(n)])
+        assert np.array_equal(np.sort(cat), np.arange(nx * ny, dtype=np.uint32))
+        if n > 1 and nx * ny > 16 * 16 * n:
+            assert cnt.max() - cnt.min() <= 2 * 16 * 16 * max(1, (nx + 15) // 16 // n + 1)
+
+
+def test_env_hooks_are_documented():
+    """The library reads only the test / fault hooks INTEGRATION.md lists (round 6 pruned the losing split
+    curve extend's switches and RTAMD_FUSE_BATCH; RTAMD_DEBUG_DEPTH only in the RT_STATS build)."""
+    csrc = os.path.join(ROOT, "scheme-raytrace_amd", "csrc")
+    names = set()
+    for f in ("rt_api.cpp", "rt_kernels.hip"):
+        names |= set(re.findall(r'getenv\("(RTAMD_[A-Z0-9_]+)"\)', open(os.path.join(csrc, f)).read()))
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc[doc.index("Test hooks that remain environment variables"):doc.index("Errors: every entry point")]
+    listed = set(re.findall(r"`(RTAMD_[A-Z0-9_]+)`", sec.split("Round 6")[0]))
+    assert names - {"RTAMD_DEBUG_DEPTH"} == listed, (sorted(names), sorted(listed))
+    for gone in ("RTAMD_CURVE_SPLIT", "RTAMD_CURVE_K", "RTAMD_FUSE_BATCH", "RTAMD_CURVE_DEBUG"):
+        assert gone not in names
 
 
 def test_resolve_matches_reference_formula(oracle_mod):
@@ -223,7 +273,7 @@ def test_c_example_builds_against_the_abi(tmp_path):
     import subprocess
     exe = _build_c_example(tmp_path)
     out = subprocess.run([str(exe), "--abi"], check=True, capture_output=True, text=True).stdout
-    assert out.strip() == "rt_abi_version 6"
+    assert out.strip() == "rt_abi_version 7"
 
 
 def test_load_points_and_points_to_bezier(tmp_path):
