@@ -481,6 +481,7 @@ def main():
         "constructors_ms": round(t_commit * 1e3 - info0["commit_ms"], 1),
         "commit_build_ms": round(info0["commit_ms"] - info0["commit_upload_ms"], 1),
         "commit_upload_ms": round(info0["commit_upload_ms"], 1),
+        "commit_sah_ms": round(info0["commit_sah_ms"], 1), "commit_threads": int(info0["commit_threads"]),
         "note": "one-time per scene, outside the timed steps (SURVEY §8(d) d1): scene_build = the host's scene "
                 "constructors (rtamd.scenes, e.g. points->bezier for C5); constructors = their rt_add_* calls "
                 "through the C ABI; commit_build = rt_scene_commit's flattening and BVH builds (SAH sweep, "

@@ -329,6 +329,9 @@ typedef struct rt_scene_info {
     int32_t  curve_stack;     /* curve trees: stack entries the BVH4 walk of k_extend_curves may hold (0: none) */
     double   commit_ms;       /* rt_scene_commit's wall time: flattening, BVH builds (SAH, BVH4 collapse), upload */
     double   commit_upload_ms; /* of it: device allocations and host-to-device copies */
+    double   commit_sah_ms;   /* of it: the SAH builds of the world BVH (on commit_threads host threads) */
+    int32_t  commit_threads;  /* host threads the SAH builds may use (the process's CPUs, at most 16) */
+    int32_t  reserved0;
 } rt_scene_info;
 int rt_get_scene_info(int scene, rt_scene_info* out);
 /* Record per-kernel HIP events during renders (adds a little host overhead). */

@@ -198,6 +198,8 @@ struct Scene {
     bool profiling = false;
     rt_stats stats{};
     double commit_ms = 0.0, commit_upload_ms = 0.0;   // rt_scene_commit: wall time, of it device allocation + copies
+    double commit_sah_ms = 0.0;                        // ... and the SAH builds (commit_threads host threads)
+    int commit_threads = 1;
 };
 
 // A multi-GPU frame's communicator (rt_comm_create): one RCCL rank per process, bound to a context's
@@ -503,7 +505,10 @@ int commit_scene(Scene* s, int world) {
         bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
                                      std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));
         bb.threads = build_threads();
+        s->commit_threads = bb.threads;
+        const auto ts = std::chrono::steady_clock::now();
         bb.build(0, (int)refs.size(), 0);
+        s->commit_sah_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
         // leaf ranges: refs order -> sphere / moving-sphere / curve array indices
         std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0), nb(refs.size() + 1, 0);
         for (size_t i = 0; i < refs.size(); ++i) {
@@ -595,7 +600,9 @@ int commit_scene(Scene* s, int world) {
             b0.sweep_max = bb.sweep_max;
             b0.singles = b0.leaf_max == 1;           // direct leaves (below) need one sphere per leaf
             b0.threads = bb.threads;
+            const auto t0s = std::chrono::steady_clock::now();
             b0.build(0, (int)refs0.size(), 0);
+            s->commit_sah_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0s).count();
             // fsph in refs0 order; each entry remembers which sphere / moving sphere it is
             for (const PrimRef& r : refs0) {
                 const size_t i = (size_t)r.leaf;
@@ -1881,6 +1888,8 @@ int rt_get_scene_info(int scene, rt_scene_info* out) {
     out->curve_stack = d.bvh4 ? d.stack4 : 0;
     out->commit_ms = s->commit_ms;
     out->commit_upload_ms = s->commit_upload_ms;
+    out->commit_sah_ms = s->commit_sah_ms;
+    out->commit_threads = s->commit_threads;
     return 0;
 }
 

@@ -274,10 +274,10 @@ inline int32_t collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, st
     // iterative: (bvh2 node, bvh4 index) pairs still to fill
     std::vector<std::pair<int32_t, int32_t>> todo{{root, 0}};
     std::vector<int32_t> need;                     // per bvh4 node: children - 1
-    std::vector<std::vector<int32_t>> kids;        // per bvh4 node: inner bvh4 children
+    std::vector<int32_t> parent;                   // per bvh4 node: its parent (-1: the root)
     bvh4.assign(1, BvhNode4{});
     need.assign(1, 0);
-    kids.assign(1, {});
+    parent.assign(1, -1);
     while (!todo.empty()) {
         const auto [p, q] = todo.back();
         todo.pop_back();
@@ -299,8 +299,7 @@ inline int32_t collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, st
                 const int32_t q2 = (int32_t)bvh4.size();
                 bvh4.push_back(BvhNode4{});
                 need.push_back(0);
-                kids.push_back({});
-                kids[q].push_back(q2);
+                parent.push_back(q);
                 todo.push_back({sl[j].ref, q2});
                 N.ref[j] = q2;
             } else {
@@ -311,12 +310,11 @@ inline int32_t collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, st
         bvh4[q] = N;
         need[q] = n - 1;
     }
-    // children were appended after their parents: fold the stack bound bottom-up
-    std::vector<int32_t> deep(bvh4.size(), 0);
+    // children were appended after their parents: fold the stack bound bottom-up (deepest child into the parent)
+    std::vector<int32_t> deep(bvh4.size(), 0), below(bvh4.size(), 0);
     for (size_t q = bvh4.size(); q-- > 0;) {
-        int32_t m = 0;
-        for (int32_t c : kids[q]) m = std::max(m, deep[c]);
-        deep[q] = need[q] + m;
+        deep[q] = need[q] + below[q];
+        if (parent[q] >= 0) below[parent[q]] = std::max(below[parent[q]], deep[q]);
     }
     stack4 = deep[0];
     return 0;

@@ -57,7 +57,8 @@ class RtSceneInfo(ctypes.Structure):
                [(n, ctypes.c_uint32) for n in ("extend_lds_bytes", "extend_lds_blocks", "camera_lds_bytes",
                                                "camera_lds_blocks")] + \
                [("cus", ctypes.c_int32), ("curve_stack", ctypes.c_int32), ("commit_ms", ctypes.c_double),
-                ("commit_upload_ms", ctypes.c_double)]
+                ("commit_upload_ms", ctypes.c_double), ("commit_sah_ms", ctypes.c_double),
+                ("commit_threads", ctypes.c_int32), ("reserved0", ctypes.c_int32)]
 
 
 # name -> argtypes (restype is always c_int status, except where noted)
