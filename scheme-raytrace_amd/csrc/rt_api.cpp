@@ -184,7 +184,7 @@ struct Scene {
     DevScene dev{};
     DevBuf d_sph, d_msph, d_rect, d_bez, d_klein, d_med, d_bgroups, d_groups, d_chains, d_leaves, d_mats, d_texs, d_ranvec, d_perm, d_bvh2, d_bleaf;
     DevBuf d_fbvh2, d_fbleaf, d_fsph, d_fid;      // time-0 BVH (commit_scene)
-    DevBuf d_bvh4, d_stk_ovf, d_bez_ring;                      // curve trees: BVH4 and the walk's stack overflow
+    DevBuf d_bvh4, d_stk_ovf, d_bez_ring, d_fuse_ring;         // curve trees: BVH4, the walk's stack overflow, rings
     DevBuf d_dev;                                  // a device copy of `dev` (kernels that take the scene by pointer)
     DevBuf d_leaf_cls;
     size_t ext_lds = 0;                            // k_extend_lds: LDS bytes (0 = not used) and grid cap
@@ -394,7 +394,15 @@ double scene_radius(const Scene* s, const Flattener& f) {
 
 size_t extend_lds_budget() { return (size_t)64 << 10; }   // largest LDS footprint k_extend_lds may take
 
+#ifdef RT_COMMIT_PROFILE
+#define COMMIT_MARK(tag) std::fprintf(stderr, "commit %-12s %9.1f ms\n", tag, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - cp0).count())
+#else
+#define COMMIT_MARK(tag) ((void)0)
+#endif
 int commit_scene(Scene* s, int world) {
+#ifdef RT_COMMIT_PROFILE
+    const auto cp0 = std::chrono::steady_clock::now();
+#endif
     Context* c = get_ctx(s->ctx);
     if (!c) return fail("scene's context was destroyed");
     HIPCHK(hipSetDevice(c->device));
@@ -442,6 +450,7 @@ int commit_scene(Scene* s, int world) {
     }
 
     // BVH over the world-level (chain -1) spheres, moving spheres and curves of segment 0
+    COMMIT_MARK("flatten");
     std::vector<PrimRef> refs;
     for (size_t i = 0; i < f.leaves.size(); ++i) {
         const LeafTmp& L = f.leaves[i];
@@ -478,6 +487,7 @@ int commit_scene(Scene* s, int world) {
         for (int k = 0; k < 3; ++k) r.c[k] = 0.5 * (r.lo[k] + r.hi[k]);
         refs.push_back(r);
     }
+    COMMIT_MARK("refs");
     const bool use_bvh = !refs.empty() && refs.size() >= bvh_min_prims();
     std::vector<BvhNode> bvh_nodes;
     std::vector<BvhNode2> bvh2;
@@ -509,6 +519,7 @@ int commit_scene(Scene* s, int world) {
         const auto ts = std::chrono::steady_clock::now();
         bb.build(0, (int)refs.size(), 0);
         s->commit_sah_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+        COMMIT_MARK("sah");
         // leaf ranges: refs order -> sphere / moving-sphere / curve array indices
         std::vector<int> ns(refs.size() + 1, 0), nm(refs.size() + 1, 0), nb(refs.size() + 1, 0);
         for (size_t i = 0; i < refs.size(); ++i) {
@@ -535,7 +546,9 @@ int commit_scene(Scene* s, int world) {
             };
             for (BvhNode2& M : bvh2) { direct(M.l); direct(M.r); }
             direct(bvh2_root);
+            COMMIT_MARK("bvh2");
             bvh4_root = collapse_bvh4(bvh2, bvh2_root, bvh4, stack4);
+            COMMIT_MARK("bvh4");
         }
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
         for (const PrimRef& r : refs) {
@@ -635,6 +648,7 @@ int commit_scene(Scene* s, int world) {
             }
         }
     }
+    COMMIT_MARK("records");
     std::vector<MediumRec> med;
     std::vector<LeafInfo> lmed;
     std::vector<Group> bgroups;
@@ -791,6 +805,7 @@ int commit_scene(Scene* s, int world) {
     }
     DevScene& d = s->dev;
     std::memset(&d, 0, sizeof d);
+    COMMIT_MARK("groups");
     if (int rc = upload(s->d_sph, sph, &d.sph)) return rc;
     if (int rc = upload(s->d_msph, msph, &d.msph)) return rc;
     if (int rc = upload(s->d_rect, rect, &d.rect)) return rc;
@@ -842,6 +857,8 @@ int commit_scene(Scene* s, int world) {
             d.ring_waves = (uint32_t)std::max(cus, 1) * 4u * (uint32_t)RT_CURVE_WAVES;
             HIPCHK(s->d_bez_ring.ensure((size_t)kLanes * d.ring_waves * kBezRing * 128u));
             d.bez_ring = s->d_bez_ring.as<double>();
+            HIPCHK(s->d_fuse_ring.ensure((size_t)kLanes * d.ring_waves * kFuseWaveBytes));
+            d.fuse_ring = s->d_fuse_ring.as<uint8_t>();
         }
         if (stack4 > d.lds4) {                       // the walk's deepest stacks spill past the LDS columns
             int dev = 0, cus = 0;
@@ -930,6 +947,7 @@ int commit_scene(Scene* s, int world) {
         (void)hipGetLastError();
     }
     HIPCHK(s->d_dev.ensure(sizeof(DevScene)));
+    COMMIT_MARK("upload");
     HIPCHK(hipMemcpy(s->d_dev.p, &d, sizeof(DevScene), hipMemcpyHostToDevice));
     s->committed = true;
     return 0;
@@ -1065,6 +1083,7 @@ int lanes_for(const Context& c, const DevScene& d) {
 constexpr uint32_t kFuseMaxRays = 1u << 24;
 bool curve_fuse(const DevScene& d, const uint32_t n) {
     if (!(curve_kernel_scene(d) && curve_persistent() && !d.has_perlin && d.light.type == LIGHT_OFF)) return false;
+    if (!d.fuse_ring || d.n_leaves >= (1 << kFuseLeafBits) - 1) return false;    // FuseHit packs leaf + 1 in 25 bits
     const char* e = std::getenv("RTAMD_CURVE_FUSE");   // read per render: tests switch it inside one process
     if (e && e[0] == '0') return false;
     if (e && e[0] == '1') return true;
@@ -1236,8 +1255,11 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
         }
     } drain{c, nlanes};
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    // RT_OPT_EXACT_LIBM: auto = exact in scenes with curves ("libm")
-    const bool exact_libm = c->opt_exact_libm == RT_LIBM_EXACT || (c->opt_exact_libm == RT_LIBM_AUTO && s->dev.n_bez > 0);
+    // RT_OPT_EXACT_LIBM: auto = exact in scenes with curves or noise / marble textures ("libm"):
+    // C3 (marble) frame rows with the device library's sin / cos were 0.79 % of pixels off by more than 1e-9;
+    // exact there costs 1.7 % (profiles/r06/c3_libm/), against 5.5 % on the cover scene, which keeps the device's
+    const bool exact_libm = c->opt_exact_libm == RT_LIBM_EXACT ||
+                            (c->opt_exact_libm == RT_LIBM_AUTO && (s->dev.n_bez > 0 || s->dev.has_noise_tex));
     uint64_t seq = 0;
 
     // Enqueue the lane's next step for its current path count: one wavefront
@@ -1282,6 +1304,7 @@ int render_impl(Scene* s, int nx, int ny, const PixSel& ps, int spp_begin, int s
             DevScene dl = s->dev;
             if (dl.stk_ovf) dl.stk_ovf += (size_t)L.index * dl.ovf_lanes * (size_t)(dl.stack4 - dl.lds4);
             if (dl.bez_ring) dl.bez_ring += (size_t)L.index * dl.ring_waves * kBezRing * 16u;
+            if (dl.fuse_ring) dl.fuse_ring += (size_t)L.index * dl.ring_waves * kFuseWaveBytes;
             // the fused curve extend (k_extend_curves<FUSE>): every depth from 1 on in this one launch
             CurveFuse fz{L.seg_tail.as<unsigned long long>() + 3, (uint32_t)L.depth};
             fused = L.depth > 0 && curve_fuse(s->dev, L.n);

@@ -161,6 +161,10 @@ struct DevScene {
     // k_extend_curves' survivor rings: per resident wave kBezRing entries of 128 B (a root-culled curve's
     // ray-space control points and widths, written by stage A, read by stage B's refills and takes)
     double* bez_ring;  uint32_t ring_waves;
+    // the fused curve extend's per-wave hand-off rings (k_extend_curves<FUSE>): kFuseRing parked hits
+    // (FuseHit, waiting for a whole-wave shading round) then kFuseRing ready paths (FuseReady, scattered
+    // rays waiting for a lane), kFuseWaveBytes per resident wave
+    uint8_t* fuse_ring;
     int32_t bvh4_root, stack4;
     int32_t lds4;                                  // the walk's stack entries in LDS (lane_stack; tests lower it)
     uint32_t* stk_ovf;     uint32_t ovf_lanes;
@@ -246,6 +250,17 @@ constexpr int kShards = 8;
 #endif
 constexpr int kCntStride = RT_CNT_STRIDE;
 struct QView { const uint32_t* counts; uint32_t cap; };
+
+// The fused curve extend's hand-off records (DevScene::fuse_ring).  A lane whose ray is resolved parks
+// its hit (slot, leaf + 1 with the path depth above it, closest t); once a wave has 64 parked, every lane
+// shades one (a whole-wave round) and the paths that go on are listed as ready (slot, depth) for the next
+// free lanes.  A wave owns at most 64 walking + 63 parked paths when it claims new ones (and claims only
+// with no ready path left), so 128 entries per ring cannot overflow; kFuseRing leaves a margin.
+struct alignas(16) FuseHit { uint32_t slot, leaf_dep; double t; };      // leaf_dep = (leaf + 1) | depth << 25
+struct alignas(8) FuseReady { uint32_t slot, depth; };
+constexpr int kFuseRing = 256;
+constexpr size_t kFuseWaveBytes = (size_t)kFuseRing * (sizeof(FuseHit) + sizeof(FuseReady));
+constexpr int kFuseLeafBits = 25;                                    // leaves below 2^25 - 1 (launch_extend checks)
 
 // The fused curve extend's launch (launch_extend, k_extend_curves<FUSE>): every depth from `depth` on in
 // one launch; continuation segments are counted into *segs

@@ -1904,12 +1904,15 @@ static_assert(4 * sizeof(BezWave) + 256 * sizeof(uint32_t) * RT_CURVE_LDS_STACK 
 #ifndef RT_CURVE_PREFETCH
 #define RT_CURVE_PREFETCH 1            // load the lane's next BVH4 node one iteration ahead (32 VGPRs)
 #endif
-// FUSE (1: device libm, 2: the exact libm): every depth from fz.depth on in one launch.  A lane
-// whose ray is resolved shades it on the spot (shade_hit, the wavefront shade's own code: any material,
-// no Perlin tables, no light mixture — launch_extend checks the scene) and, if the path goes on, stores
-// the scattered ray in place (same slot) and walks it at once, so the launch drains once per chunk
-// instead of once per depth (C5: ~1.1 ms per depth launch, about a quarter of the curve kernel's time).
-// Paths that end write their sample; continuation segments are counted into *fz.segs.
+// FUSE (1: device libm, 2: the exact libm): every depth from fz.depth on in one launch, so the launch
+// drains once per chunk instead of once per depth (C5: ~1.1 ms per depth launch).  A lane whose ray is
+// resolved parks its hit in the wave's hand-off ring (FuseHit) and takes the next ray at once; when 64
+// hits are parked, every lane of the wave shades one (shade_hit, the wavefront shade's own code: any
+// material, no Perlin tables, no light mixture — launch_extend checks the scene), whatever its own walk
+// is doing, so shading runs on whole waves (round 5 shaded on the ~20 lanes of a finishing batch).  A
+// scattered path is stored in place (same slot) and listed as ready (FuseReady); free lanes take ready
+// paths before new rays.  Paths that end write their sample; continuation segments are counted into
+// *fz.segs.
 template <bool EX>
 __device__ __forceinline__ bool fused_shade(const DevScene& sc, const RenderParams& rp, PathRegs& p, const double t,
                                             const int32_t leaf, v3& L);   // below shade_hit
@@ -1988,6 +1991,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
     BezRoot* const ring = reinterpret_cast<BezRoot*>(sc.bez_ring) +
                           (size_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) * (size_t)kBezRing;
     uint32_t rtail = 0;
+    // FUSE: the wave's hand-off rings (parked hits, ready paths; wave-uniform heads and tails)
+    FuseHit* const pk = FUSE ? reinterpret_cast<FuseHit*>(sc.fuse_ring + (size_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) *
+                                                          kFuseWaveBytes) : nullptr;
+    FuseReady* const rd = reinterpret_cast<FuseReady*>(pk + kFuseRing);
+    uint32_t pk_head = 0, pk_tail = 0, rd_head = 0, rd_tail = 0;
     // a ray takes at most one step per node / leaf and one queue step per two curves: bound its
     // working iterations (a valid walk stays far below)
     const uint32_t ray_cap = g_curve_ray_cap ? g_curve_ray_cap : 4u * (uint32_t)(sc.n_bvh2 + sc.n_bleaf + sc.n_bez) + 4096u;
@@ -2028,27 +2036,54 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
         const bool flush = fin_m != 0ull && (exhausted || __popcll(fin_m) >= RT_CURVE_FINISH_BATCH ||
                                              fin_m == __ballot(active));
         if constexpr (FUSE != 0) {
-            if (fin && flush) {                              // shade here; a scattered path goes on in this lane
-                PathRegs p;
-                load_path(st, i, p, rp, dep);
-                for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<0>(sc, sc.groups[g], p.o, p.d, p.time, closest, best, nullptr);
-                v3 L;
+            // park every resolved ray at once (its lane takes the next one in step 2)
+            if (fin) {
+                pk[(pk_tail + lanes_below(fin_m)) & (uint32_t)(kFuseRing - 1)] =
+                    FuseHit{i, (uint32_t)(best + 1) | (dep << kFuseLeafBits), closest};
+                active = false;
+            }
+            pk_tail += (uint32_t)__popcll(fin_m);
+            // a shading round: 64 parked hits, or — once no new rays are left and no ready path waits — the
+            // ones there are, when the finishing batch's share of the wave is idle or the wave is drained
+            const uint32_t npk = pk_tail - pk_head;
+            bool round = npk >= 64u;
+            if (!round && npk > 0u && exhausted && rd_head == rd_tail) {
+                const unsigned long long am = __ballot(active);
+                round = am == 0ull || __popcll(__ballot(!active && !dead)) >= RT_CURVE_FINISH_BATCH;
+            }
+            if (round) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the parked hits other lanes wrote
+                wave_sync();
+                const uint32_t take = npk < 64u ? npk : 64u;
                 bool go = false;
-                if (best < 0) L = sky_radiance(sc, p.d);
-                else go = fused_shade<FUSE == 2>(sc, rp, p, closest, best, L);
-                if (go) {
-                    store_path(st, i, p);
-                    dep = p.depth;
-                    ++fsegs;
-                    start_ray();
-                    W.done[lane] = 0u;
-                    queued = 0u;
-                    pb = pe = 0;
-                    ray_it = 0;
-                } else {
-                    write_sample(rp, p, L);
-                    active = false;
+                uint32_t gslot = 0, gdep = 0;
+                if (lane < take) {
+                    const FuseHit h = pk[(pk_head + lane) & (uint32_t)(kFuseRing - 1)];
+                    double t = h.t;
+                    int32_t leaf = (int32_t)(h.leaf_dep & ((1u << kFuseLeafBits) - 1u)) - 1;
+                    PathRegs p;
+                    load_path(st, h.slot, p, rp, h.leaf_dep >> kFuseLeafBits);
+                    for (int g = gb + 1; g < sc.n_groups; ++g) group_closest<0>(sc, sc.groups[g], p.o, p.d, p.time, t, leaf, nullptr);
+                    v3 L;
+                    if (leaf < 0) L = sky_radiance(sc, p.d);
+                    else go = fused_shade<FUSE == 2>(sc, rp, p, t, leaf, L);
+                    if (go) {
+                        store_path(st, h.slot, p);
+                        gslot = h.slot;
+                        gdep = p.depth;
+                        ++fsegs;
+                    } else {
+                        write_sample(rp, p, L);
+                    }
                 }
+                pk_head += take;
+                const unsigned long long gm = __ballot(go);
+                if (go) rd[(rd_tail + lanes_below(gm)) & (uint32_t)(kFuseRing - 1)] = FuseReady{gslot, gdep};
+                rd_tail += (uint32_t)__popcll(gm);
+                if (rd_tail - rd_head > (uint32_t)kFuseRing || pk_tail - pk_head > (uint32_t)kFuseRing)
+                    raise_fault(RT_FAULT_PATH);                  // cannot happen (FuseHit, rt_device.h)
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the paths and ready entries just stored
+                wave_sync();
             }
         } else if (fin && flush) {
             if (gb + 1 < sc.n_groups || best < 0) {          // the groups after the BVH or the sky: the ray again
@@ -2085,8 +2120,29 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk1 += t - st_t; st_t = t; }
 #endif
-        // 2. free lanes take the next rays (claimed positions in the input queue)
-        const unsigned long long need = __ballot(!active && !dead);
+        // 2. free lanes take the next rays: FUSE, the wave's ready paths first; then claimed positions in the
+        //    input queue
+        unsigned long long need = __ballot(!active && !dead);
+        if constexpr (FUSE != 0) {
+            const uint32_t nrd = rd_tail - rd_head;
+            if (need && nrd) {
+                const uint32_t cnt = (uint32_t)__popcll(need), take = cnt < nrd ? cnt : nrd;
+                const uint32_t r = lanes_below(need);
+                if (!active && !dead && r < take) {
+                    const FuseReady e = rd[(rd_head + r) & (uint32_t)(kFuseRing - 1)];
+                    i = e.slot;
+                    dep = e.depth;
+                    start_ray();
+                    W.done[lane] = 0u;
+                    queued = 0u;
+                    pb = pe = 0;
+                    active = true;
+                    ray_it = 0;
+                }
+                rd_head += take;
+                need = __ballot(!active && !dead);
+            }
+        }
         if (need && !exhausted) {
             const uint32_t cnt = (uint32_t)__popcll(need);
             const int leader = __ffsll((long long)need) - 1;
@@ -2110,7 +2166,11 @@ __global__ __launch_bounds__(256, RT_CURVE_WAVES) void k_extend_curves(const Dev
                 }
             }
         }
-        if (__ballot(active) == 0ull) break;         // every queued candidate has been resolved
+        if (__ballot(active) == 0ull) {              // every queued candidate has been resolved
+            if constexpr (FUSE == 0) break;
+            // FUSE: done once nothing is parked or ready (or no lane is left to take a path: a fault)
+            if ((exhausted && pk_head == pk_tail && rd_head == rd_tail) || __ballot(!dead) == 0ull) break;
+        }
 #ifdef RT_STATS
         { const unsigned long long t = __builtin_amdgcn_s_memtime(); st_clk2 += t - st_t; st_t = t; }
 #endif

@@ -22,8 +22,8 @@ RT_SKY_GRADIENT, RT_SKY_BLACK = 0, 1
 RT_RECT_XY, RT_RECT_XZ, RT_RECT_YZ = 0, 1, 2
 #: render-schedule options of a context (include/rt.h RT_OPT_*; 0 = automatic)
 RT_OPTIONS = {"lanes": 1, "max_paths": 2, "tail_paths": 3, "tail_div": 4, "tail_off": 5, "exact_libm": 6}
-#: RT_OPT_EXACT_LIBM values: auto (exact in scenes with curves), exact (the C library's sin / cos bit for
-#: bit), device (the device library's)
+#: RT_OPT_EXACT_LIBM values: auto (exact in scenes with curves or noise / marble textures), exact (the C
+#: library's sin / cos bit for bit), device (the device library's)
 RT_LIBM = {"auto": 0, "exact": 1, "device": 2}
 RT_COMM_ID_BYTES = 128
 

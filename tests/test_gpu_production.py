@@ -129,22 +129,24 @@ def test_config_band_production_vs_oracle(sched, oracle_mod, name):
 @pytest.mark.parametrize("name", ["cover", "cover_marble"])
 def test_horizon_rows_exact_libm(sched, oracle_mod, name):
     """C2 / C3 frame rows 536..543 (the horizon band of the 1920x1080 frame, where the bench's parity_frame
-    rows sit), passes 0..63, production schedule (8 chunks on 2 lanes).  With RT_OPT_EXACT_LIBM = exact
+    rows sit), passes 0..255, production schedule (8 chunks on 2 lanes).  With RT_OPT_EXACT_LIBM = exact
     the bounce directions' sin / cos are the C library's bit for bit, and the image must equal the oracle's
-    to the last bits: 0 pixels off by more than 1e-9.  The default mode (the device library's sin / cos in
-    scenes without curves) is rendered too, and its count printed."""
+    to the last bits: 0 pixels off by more than 1e-9.  The default mode (round 6: exact in scenes with
+    noise / marble textures, so C3's count is 0; the device library's sin / cos in the cover scene) may
+    move at most 0.5 % of the pixels by more than 1e-9."""
     import torch
-    nx, ny, y0, rows, n = 1920, 1080, 536, 8, 64
+    nx, ny, y0, rows, n = 1920, 1080, 536, 8, 256
     scene = scenes.SCENES[name](nx, ny)
     lo, hi = y0 * nx, (y0 + rows) * nx
     ref = np.zeros(nx * ny * 3)
     oracle_mod.build_scene(scene).render(nx, ny, 0, n, SEED, ref, lo, hi, nthreads=host_threads())
-    sched.set_option("max_paths", 8 * rows * nx)
+    sched.set_option("max_paths", 32 * rows * nx)
     sched.set_option("lanes", 2)
     res = {}
     for mode in ("exact", "auto"):
         sched.set_option("exact_libm", mode)
         acc = torch.zeros(nx * ny * 3, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
         h = gpu.render_rows_device(scene, nx, ny, y0, rows, 0, n, SEED, acc.data_ptr())
         st = gpu.stats(h)
         assert st.chunks >= 4 and st.lanes == 2 and st.extend_rays > st.paths
@@ -153,7 +155,9 @@ def test_horizon_rows_exact_libm(sched, oracle_mod, name):
               % (name, y0, y0 + rows - 1, n - 1, mode, *res[mode]))
     rms, dmax, nbad, npx = res["exact"]
     assert nbad == 0 and rms <= 1e-12, res["exact"]
-    assert res["auto"][0] <= RMS_TOL
+    assert res["auto"][0] <= RMS_TOL and res["auto"][2] <= npx // 200, res["auto"]
+    if name == "cover_marble":
+        assert res["auto"][2] == 0, res["auto"]
 
 
 def test_exact_libm_option_values(sched):
