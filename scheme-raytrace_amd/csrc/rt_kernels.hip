@@ -318,7 +318,16 @@ __device__ __forceinline__ v3 bez_point(const Bez4& c, const double t) {       /
     const double u = 1.0 - t, u2 = u * u, u3 = u2 * u;
     return ((c.p0 * u3 + c.p1 * (3.0 * u2 * t)) + c.p2 * (3.0 * u * t2)) + c.p3 * t3;
 }
-__device__ __forceinline__ v3 half_div(const v3 a, const v3 b) { return a * 0.5 + b * 0.5; }   // :45-47, t = 0.5
+#ifndef RT_BEZ_HALFSUM
+#define RT_BEZ_HALFSUM 0
+#endif
+__device__ __forceinline__ v3 half_div(const v3 a, const v3 b) {   // internally-divide :45-47 at t = 0.5
+#if RT_BEZ_HALFSUM
+    return (a + b) * 0.5;
+#else
+    return a * 0.5 + b * 0.5;
+#endif
+}
 __device__ __forceinline__ void bez_split(const Bez4& c, Bez4& l, Bez4& r) {    // split :78-87
     const v3 sp = bez_point(c, 0.5);
     const v3 nbc = half_div(c.p1, c.p2);
