@@ -551,32 +551,40 @@ int commit_scene(Scene* s, int world) {
             COMMIT_MARK("bvh4");
         }
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
-        for (const PrimRef& r : refs) {
-            const LeafTmp& L = f.leaves[r.leaf];
-            const Obj& o = s->objs[L.obj];
-            LeafInfo li{};
-            li.type = L.type; li.chain = -1; li.mat = o.mat; li.flip = L.flip;
-            if (r.type == LEAF_SPHERE) {
-                li.inv_r = 1.0 / o.r; 
-                li.local = (int)sph.size();
-                sph.push_back({o.c0[0], o.c0[1], o.c0[2], o.r * o.r});
-                lsph.push_back(li);
-            } else if (r.type == LEAF_MSPHERE) {
-                li.inv_r = 1.0 / o.r; 
-                li.local = (int)msph.size();
-                MSphereRec m{};
-                m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
-                m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
-                m.t0 = o.t0; m.den = o.t1 - o.t0;
-                msph.push_back(m);
-                lmsph.push_back(li);
-            } else {
-                li.local = (int)bez.size();
-                bez.push_back(bezier_rec(o));
-                bez.back().order = (uint32_t)r.leaf;          // the flattened list position
-                lbez.push_back(li);
+        // records in refs order: ref i is sphere ns[i] / moving sphere nm[i] / curve nb[i] of its type's
+        // arrays (the prefix counts above), so the refs fill them independently, on the build's threads
+        sph.resize((size_t)ns[refs.size()]); lsph.resize(sph.size());
+        msph.resize((size_t)nm[refs.size()]); lmsph.resize(msph.size());
+        bez.resize((size_t)nb[refs.size()]); lbez.resize(bez.size());
+        parallel_for(refs.size(), bb.threads, [&](const size_t b, const size_t e) {
+            for (size_t i = b; i < e; ++i) {
+                const PrimRef& r = refs[i];
+                const LeafTmp& L = f.leaves[r.leaf];
+                const Obj& o = s->objs[L.obj];
+                LeafInfo li{};
+                li.type = L.type; li.chain = -1; li.mat = o.mat; li.flip = L.flip;
+                if (r.type == LEAF_SPHERE) {
+                    li.inv_r = 1.0 / o.r;
+                    li.local = ns[i];
+                    sph[(size_t)ns[i]] = SphereRec{o.c0[0], o.c0[1], o.c0[2], o.r * o.r};
+                    lsph[(size_t)ns[i]] = li;
+                } else if (r.type == LEAF_MSPHERE) {
+                    li.inv_r = 1.0 / o.r;
+                    li.local = nm[i];
+                    MSphereRec m{};
+                    m.c0x = o.c0[0]; m.c0y = o.c0[1]; m.c0z = o.c0[2]; m.rr = o.r * o.r;
+                    m.dcx = o.c1[0] - o.c0[0]; m.dcy = o.c1[1] - o.c0[1]; m.dcz = o.c1[2] - o.c0[2];
+                    m.t0 = o.t0; m.den = o.t1 - o.t0;
+                    msph[(size_t)nm[i]] = m;
+                    lmsph[(size_t)nm[i]] = li;
+                } else {
+                    li.local = nb[i];
+                    bez[(size_t)nb[i]] = bezier_rec(o);
+                    bez[(size_t)nb[i]].order = (uint32_t)r.leaf;      // the flattened list position
+                    lbez[(size_t)nb[i]] = li;
+                }
             }
-        }
+        });
         // Time-0 BVH.  Every scattered ray has time 0 (make-ray, ray.scm:8-9,
         // Q4), so for those rays a moving sphere sits at center(0) exactly:
         // the second tree bounds each moving sphere at that one position
@@ -748,6 +756,7 @@ int commit_scene(Scene* s, int world) {
         return fail("internal: leaf records and leaf infos out of step");
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
     std::vector<LeafInfo> leaves;
+    leaves.reserve(lsph.size() + lmsph.size() + rect.size() + lbez.size() + lmed.size() + lklein.size());
     int32_t base[kLeafTypes];
     base[LEAF_SPHERE] = 0;
     for (auto& li : lsph) leaves.push_back(li);

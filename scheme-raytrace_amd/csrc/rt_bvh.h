@@ -41,6 +41,20 @@ inline int build_threads() {
     return std::min(n, 16);
 }
 
+// f(b, e) over [0, n) cut into `threads` contiguous ranges, one host thread each (small n: inline)
+template <class F>
+inline void parallel_for(const size_t n, const int threads, F f) {
+    if (threads <= 1 || n < 65536) { f((size_t)0, n); return; }
+    const size_t chunk = (n + (size_t)threads - 1) / (size_t)threads;
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) {
+        const size_t b = (size_t)t * chunk, e = std::min(n, b + chunk);
+        if (b < e) th.emplace_back(f, b, e);
+    }
+    f((size_t)0, std::min(n, chunk));
+    for (std::thread& x : th) x.join();
+}
+
 // The builder.  build() appends nodes in depth-first preorder (a node, its left subtree, its right
 // subtree); a subtree's shape depends only on its own primitives, which it reorders within its own range
 // [b, e) of refs.  So subtrees of at least kGrain primitives can be built by other threads into vectors of
@@ -234,6 +248,8 @@ template <class LeafFn>
 inline void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_of, std::vector<BvhNode2>& bvh2,
                   std::vector<BvhLeaf>& bleaf, int32_t& root, int32_t& lane_stack) {
     std::vector<int> inner_idx(nodes.size(), -1), leaf_idx(nodes.size(), -1);
+    bvh2.reserve(bvh2.size() + nodes.size() / 2 + 1);
+    bleaf.reserve(bleaf.size() + nodes.size() / 2 + 1);
     for (size_t i = 0; i < nodes.size(); ++i) {
         const BvhNode& N = nodes[i];
         if (N.c == -1) { inner_idx[i] = (int)bvh2.size(); bvh2.push_back(BvhNode2{}); continue; }
@@ -278,6 +294,9 @@ inline int32_t collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, st
     bvh4.assign(1, BvhNode4{});
     need.assign(1, 0);
     parent.assign(1, -1);
+    bvh4.reserve(bvh2.size());
+    need.reserve(bvh2.size());
+    parent.reserve(bvh2.size());
     while (!todo.empty()) {
         const auto [p, q] = todo.back();
         todo.pop_back();
