@@ -451,10 +451,18 @@ int commit_scene(Scene* s, int world) {
 
     // BVH over the world-level (chain -1) spheres, moving spheres and curves of segment 0
     COMMIT_MARK("flatten");
-    std::vector<PrimRef> refs;
+    const int threads = build_threads();
+    std::vector<int> in_bvh;                         // the leaves the BVH takes, in list order
     for (size_t i = 0; i < f.leaves.size(); ++i) {
         const LeafTmp& L = f.leaves[i];
-        if (seg[i] != 0 || L.chain != -1 || (L.type != LEAF_SPHERE && L.type != LEAF_MSPHERE && L.type != LEAF_BEZIER)) continue;
+        if (seg[i] == 0 && L.chain == -1 && (L.type == LEAF_SPHERE || L.type == LEAF_MSPHERE || L.type == LEAF_BEZIER))
+            in_bvh.push_back((int)i);
+    }
+    std::vector<PrimRef> refs(in_bvh.size());
+    parallel_for(in_bvh.size(), threads, [&](const size_t jb, const size_t je) {
+      for (size_t j = jb; j < je; ++j) {
+        const size_t i = (size_t)in_bvh[j];
+        const LeafTmp& L = f.leaves[i];
         const Obj& o = s->objs[L.obj];
         PrimRef r{};
         r.leaf = (int)i;
@@ -485,8 +493,9 @@ int commit_scene(Scene* s, int world) {
         }
         pad_box(r.lo, r.hi);
         for (int k = 0; k < 3; ++k) r.c[k] = 0.5 * (r.lo[k] + r.hi[k]);
-        refs.push_back(r);
-    }
+        refs[j] = r;
+      }
+    });
     COMMIT_MARK("refs");
     const bool use_bvh = !refs.empty() && refs.size() >= bvh_min_prims();
     std::vector<BvhNode> bvh_nodes;
@@ -514,7 +523,7 @@ int commit_scene(Scene* s, int world) {
         bb.leaf_max = 1;
         bb.sweep_max = bvh_sweep_max(bb.leaf_max > 1 &&
                                      std::any_of(refs.begin(), refs.end(), [](const PrimRef& r) { return r.type == LEAF_BEZIER; }));
-        bb.threads = build_threads();
+        bb.threads = threads;
         s->commit_threads = bb.threads;
         const auto ts = std::chrono::steady_clock::now();
         bb.build(0, (int)refs.size(), 0);
@@ -537,7 +546,7 @@ int commit_scene(Scene* s, int world) {
         bvh_pad = (float)margin;
         flatten_bvh2(bvh_nodes, margin, [&](int b, int e) {
             return BvhLeaf{ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0};
-        }, bvh2, bleaf, bvh2_root, lane_stack);
+        }, bvh2, bleaf, bvh2_root, lane_stack, threads);
         if (bvh_has_bez) {                               // single-curve leaves: direct refs (kDirectCurve)
             auto direct = [&](int32_t& ref) {
                 if (ref >= 0) return;

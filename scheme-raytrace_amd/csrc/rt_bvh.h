@@ -246,7 +246,7 @@ inline void pad_box(double* lo, double* hi) {
 // [b, e).  lane_stack = deepest BVH2 level (stack entries a traversal needs).
 template <class LeafFn>
 inline void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafFn leaf_of, std::vector<BvhNode2>& bvh2,
-                  std::vector<BvhLeaf>& bleaf, int32_t& root, int32_t& lane_stack) {
+                  std::vector<BvhLeaf>& bleaf, int32_t& root, int32_t& lane_stack, const int threads = 1) {
     std::vector<int> inner_idx(nodes.size(), -1), leaf_idx(nodes.size(), -1);
     bvh2.reserve(bvh2.size() + nodes.size() / 2 + 1);
     bleaf.reserve(bleaf.size() + nodes.size() / 2 + 1);
@@ -257,17 +257,19 @@ inline void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafF
         bleaf.push_back(leaf_of(N.a, N.b));
     }
     auto ref_of = [&](int i) { return inner_idx[i] >= 0 ? inner_idx[i] : ~leaf_idx[i]; };
-    for (size_t i = 0; i < nodes.size(); ++i) {
-        if (inner_idx[i] < 0) continue;
-        BvhNode2& M = bvh2[inner_idx[i]];
-        const BvhNode& L = nodes[nodes[i].a];
-        const BvhNode& R = nodes[nodes[i].b];
-        for (int k = 0; k < 3; ++k) {
-            M.b[2 * k] = f32_down(L.lo[k] - margin); M.b[6 + 2 * k] = f32_up(L.hi[k] + margin);
-            M.b[2 * k + 1] = f32_down(R.lo[k] - margin); M.b[7 + 2 * k] = f32_up(R.hi[k] + margin);
+    parallel_for(nodes.size(), threads, [&](const size_t b, const size_t e) {    // each node on its own
+        for (size_t i = b; i < e; ++i) {
+            if (inner_idx[i] < 0) continue;
+            BvhNode2& M = bvh2[inner_idx[i]];
+            const BvhNode& L = nodes[nodes[i].a];
+            const BvhNode& R = nodes[nodes[i].b];
+            for (int k = 0; k < 3; ++k) {
+                M.b[2 * k] = f32_down(L.lo[k] - margin); M.b[6 + 2 * k] = f32_up(L.hi[k] + margin);
+                M.b[2 * k + 1] = f32_down(R.lo[k] - margin); M.b[7 + 2 * k] = f32_up(R.hi[k] + margin);
+            }
+            M.l = ref_of(nodes[i].a); M.r = ref_of(nodes[i].b);
         }
-        M.l = ref_of(nodes[i].a); M.r = ref_of(nodes[i].b);
-    }
+    });
     root = ref_of(0);
     std::vector<int> depth(nodes.size(), 0);
     for (size_t i = 0; i < nodes.size(); ++i)

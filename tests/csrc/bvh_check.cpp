@@ -169,7 +169,7 @@ static Built run(std::vector<PrimRef> refs, int threads, int sweep) {
     for (const PrimRef& r : refs) o.order.push_back(r.leaf);
     std::vector<BvhLeaf> bleaf;
     flatten_bvh2(o.nodes, 1e-6, [&](int b, int e) { return BvhLeaf{b, e - b, 0, 0, 0, 0, 0, 0}; }, o.bvh2, bleaf,
-                 o.root, o.stack);
+                 o.root, o.stack, std::is_same<B, BvhBuild>::value ? threads : 1);
     collapse_bvh4(o.bvh2, o.root, o.bvh4, o.stack4);
     return o;
 }
