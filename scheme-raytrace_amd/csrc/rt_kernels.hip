@@ -116,12 +116,15 @@ __device__ __forceinline__ double div_ia(const double x, const double a, const d
 __device__ __forceinline__ double rt_sin(const double x) { return rtlibm::sin_full(x); }
 __device__ __forceinline__ double rt_cos(const double x) { return rtlibm::cos_full(x); }
 // cos(a) and sin(b), one evaluation after the other: inlined side by side, the two would hold their
-// temporaries at once (the shade kernels' register budget)
+// temporaries at once (the shade kernels' register budget).  Bounce angles only: a, b = 2 pi u with u in
+// (0, 1) lie inside the restated reduction range (rtlibm::in_range), so the platform fallback that
+// sincos_full carries for huge arguments (the device library's Payne-Hanek path) is not compiled in —
+// it cost the lambertian shade 27 VGPRs (154 vs 127, 3 waves instead of 4)
 __device__ __forceinline__ void rt_cos_sin(const double a, const double b, double& c, double& s, const double* tab) {
     double v0 = 0.0, v1 = 0.0;
 #pragma unroll 1
     for (int j = 0; j < 2; ++j) {
-        const double v = rtlibm::sincos_full(j == 0 ? a : b, j == 0, tab);
+        const double v = rtlibm::sincos_(j == 0 ? a : b, j == 0, tab);
         if (j == 0) v0 = v; else v1 = v;
     }
     c = v0;
@@ -323,8 +326,13 @@ __device__ __forceinline__ v3 bez_point(const Bez4& c, const double t) {       /
 // same reason, so (a + b) * 0.5 gives the same bits with one multiply less per component (15 per split;
 // C5 at 8 spp +0.75 %, same image, profiles/r06/ab_halfsum/)
 __device__ __forceinline__ v3 half_div(const v3 a, const v3 b) { return (a + b) * 0.5; }
+// bez-p at t = 0.5: ((p0 0.125 + p1 0.375) + p2 0.375) + p3 0.125 (bez_point's products and sums).  The
+// products by 0.125 are exact, RN(p 0.375) = RN(3 p) / 8, and RN(x / 8 + y / 8) = RN(x + y) / 8 (scaling by
+// a power of two commutes with rounding outside the subnormal range): the same bits as
+// RN(RN(RN(p0 + RN(3 p1)) + RN(3 p2)) + p3) / 8, one operation less per component
+__device__ __forceinline__ v3 bez_mid(const Bez4& c) { return (((c.p0 + c.p1 * 3.0) + c.p2 * 3.0) + c.p3) * 0.125; }
 __device__ __forceinline__ void bez_split(const Bez4& c, Bez4& l, Bez4& r) {    // split :78-87
-    const v3 sp = bez_point(c, 0.5);
+    const v3 sp = bez_mid(c);
     const v3 nbc = half_div(c.p1, c.p2);
     const v3 lb = half_div(c.p0, c.p1);
     const v3 lc = half_div(lb, nbc);
@@ -2684,8 +2692,8 @@ __device__ __forceinline__ v3 random_to_sphere(const double radius, const double
     const double r1 = g.next();
     const double r2 = g.next();
     const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / distance_squared) - 1.0);
-    const double phi = 2.0 * kPi * r1;
-    return mk((EX ? rt_cos(phi) : cos(phi)) * sqrt(1.0 - z * z), (EX ? rt_sin(phi) : sin(phi)) * sqrt(1.0 - z * z), z);
+    const double phi = 2.0 * kPi * r1;                       // in (0, 2 pi): rt_libm.h's range, no fallback
+    return mk((EX ? rtlibm::cos_(phi) : cos(phi)) * sqrt(1.0 - z * z), (EX ? rtlibm::sin_(phi) : sin(phi)) * sqrt(1.0 - z * z), z);
 }
 template <bool EX>
 __device__ __forceinline__ v3 light_random(const DevLight& L, const v3 o, Rng& g) {
