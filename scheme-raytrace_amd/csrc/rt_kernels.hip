@@ -2907,10 +2907,15 @@ __device__ __forceinline__ void stage_perlin(const DevScene& sc, PerlinLds& P) {
 #ifndef RT_SHADE_WAVES_MD
 #define RT_SHADE_WAVES_MD 1            // metal / dielectric (memory-bound gathers)
 #endif
-template <int MAT>
-constexpr int shade_waves() { return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD : RT_SHADE_WAVES; }
+// the exact libm's lambertian kernels without Perlin tables or the light mixture (EX) at 4 waves: with the
+// bounce angles' in-range sin / cos (rt_cos_sin) they need 137 VGPRs left alone and fit 128 with no spill
+template <int MAT, bool PN, bool LS, bool EX>
+constexpr int shade_waves() {
+    return (MAT == MAT_METAL || MAT == MAT_DIELECTRIC) ? RT_SHADE_WAVES_MD
+         : (MAT == MAT_LAMBERTIAN && EX && !PN && !LS) ? 4 : RT_SHADE_WAVES;
+}
 template <int MAT, bool PN, bool LS, bool LL, bool EX>
-__global__ __launch_bounds__(256, shade_waves<MAT>()) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
+__global__ __launch_bounds__(256, (shade_waves<MAT, PN, LS, EX>())) void k_shade(const DevScene* __restrict__ scp, const RenderParams rp,
                                                                 const PathState in, const HitRec* __restrict__ hq,
                                                                 const QView qv, PathState out,
                                                                 uint32_t* __restrict__ out_counts, uint32_t shard_cap,
