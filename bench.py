@@ -86,7 +86,7 @@ def shade_bytes(hits_d0, hits, survivors):
     return (76 * hits_d0 + 96 * hits + 80 * survivors + 24 * (hits_d0 + hits - survivors))
 
 
-def shade_roofline(ms_shade, launches, hits_d0, hits, survivors, note, scene):
+def shade_roofline(ms_shade, launches, hits_d0, hits, survivors, note, scene, frame=None):
     """The shade phase (one iteration's per-material k_shade launches, HIP
     events around them) against the HBM roofline."""
     if not launches or ms_shade <= 0 or not (hits_d0 + hits):
@@ -94,7 +94,7 @@ def shade_roofline(ms_shade, launches, hits_d0, hits, survivors, note, scene):
     b = shade_bytes(hits_d0, hits, survivors)
     ach = b / (ms_shade * 1e-3) / 1e9
     hpl = (hits_d0 + hits) / launches
-    pm, _ = load_pmc("shade", scene)            # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
+    pm, _ = load_pmc("shade", scene, frame)     # PMC HBM bytes per hit (tools/profile_round.sh) x hits per launch
     traffic = round(pm["bytes_per_hit"] * hpl) if pm and pm.get("bytes_per_hit") else None
     return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -394,17 +394,20 @@ def pmc_path(kind, scene):
     return os.path.join(ROOT, "profiles", "pmc", "%s_%s.json" % (scene, kind))
 
 
-def load_pmc(kind, scene):
+def load_pmc(kind, scene, frame=None):
     """The scene's PMC summary (profiles/pmc/<scene>_<kind>.json) if it was measured on this scene with
-    these kernels, else None.  Returns (summary, path relative to the repo)."""
+    these kernels and (round 6) at this frame size and sample count (`frame` = "NXxNYxSPPspp": the schedule —
+    chunks, per-depth or fused curve launches — follows them), else None.  Returns (summary, path)."""
     path = pmc_path(kind, scene)
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         pm = json.load(f)
-    if pm.get("scene") == scene and pm.get("kernel_sha16") == kernel_sha16():
-        return pm, os.path.relpath(path, ROOT)
-    return None, None
+    if pm.get("scene") != scene or pm.get("kernel_sha16") != kernel_sha16():
+        return None, None
+    if frame is not None and (" %s," % frame) not in str(pm.get("config", "")):
+        return None, None
+    return pm, os.path.relpath(path, ROOT)
 
 
 def extend_roofline(segs, tail_segs, paths, launches, ms_ext, pm, kernels, note):
@@ -581,7 +584,8 @@ def main():
     if rank == 0:
         value = segs_all / elapsed / 1e6
         ext_kernels = extend_kernels(a.scene, gpu.scene_info(h))
-        pm, pm_src = load_pmc("extend", a.scene)    # PMC counters of these kernels (tools/profile_round.sh)
+        frame = "%dx%dx%dspp" % (nx, ny, spp)
+        pm, pm_src = load_pmc("extend", a.scene, frame)    # PMC counters of these kernels (tools/profile_round.sh)
         two_lane = None
         if iso is not None:
             roof = extend_roofline(iso.segments, iso.segments - iso.extend_rays, iso.paths,
@@ -640,13 +644,14 @@ def main():
             "roofline": roof, "roofline_two_lane": two_lane, "roofline_frame": roof_frame,
             "valu": valu, "valu_issue": valu_issue,
             "roofline_shade": (shade_roofline(iso.ms_shade, iso.extend_launches, iso.shade_hits_d0, iso.shade_hits,
-                                              iso.shade_survivors, "single render lane frame, as roofline", a.scene)
+                                              iso.shade_survivors, "single render lane frame, as roofline", a.scene,
+                                              frame)
                                if iso is not None else
                                shade_roofline(ms_shade, launches, sh_d0, sh, sh_surv, "timed region, one render lane",
-                                              a.scene)),
+                                              a.scene, frame)),
             "pmc_source": ("%s (kernels %s)" % (pm_src, pm["kernel_sha16"])) if pm else
                           "none: no PMC summary for these kernels (traffic / valu / valu_issue need "
-                          "tools/profile_round.sh on this kernel source)",
+                          "tools/profile_round.sh on this kernel source at this frame)",
             "scene_device": scene_device(gpu.scene_info(h)),
             "scene_commit": scene_commit,
             "exact_libm": a.exact_libm,
