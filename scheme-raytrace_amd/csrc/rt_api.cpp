@@ -2,11 +2,13 @@
 // of the reference's object tree into grouped leaves, device upload and the
 // wavefront driver loop (raygen → [extend → shade/compact]* → accumulate).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -15,6 +17,8 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -344,8 +348,8 @@ size_t bvh_min_prims() {
 // device time commit_scene spends in upload() (allocation + copy), for rt_scene_info's split of the
 // commit into host build and device upload
 thread_local double tl_upload_ms = 0.0;
-template <class T>
-int upload(DevBuf& b, const std::vector<T>& v, const T** out) {
+template <class T, class A>
+int upload(DevBuf& b, const std::vector<T, A>& v, const T** out) {
     const auto t0 = std::chrono::steady_clock::now();
     size_t n = std::max<size_t>(1, v.size()) * sizeof(T);
     HIPCHK(b.ensure(n));
@@ -387,12 +391,68 @@ double scene_radius(const Scene* s, const Flattener& f) {
         return r + chain_len(L.chain);
     };
     double R = n3(s->cam + 9) + std::fabs(s->cam[21]);
-    for (const LeafTmp& L : f.leaves) R = std::max(R, leaf_r(L));
+    const int nt = build_threads();
+    std::vector<double> part((size_t)nt, R);        // (max is order-free: a NaN radius never enters)
+    parallel_for(f.leaves.size(), nt, [&](const size_t b, const size_t e) {
+        double r = R;
+        for (size_t i = b; i < e; ++i) r = std::max(r, leaf_r(f.leaves[i]));
+        part[b / std::max<size_t>(1, (f.leaves.size() + (size_t)nt - 1) / (size_t)nt)] = r;
+    });
+    for (const double r : part) R = std::max(R, r);
     for (const auto& b : f.bounds) for (const LeafTmp& L : b) R = std::max(R, leaf_r(L));
     return 4 * R + 1;
 }
 
 size_t extend_lds_budget() { return (size_t)64 << 10; }   // largest LDS footprint k_extend_lds may take
+
+// A commit's host scratch (C5: ~0.7 GB of build arrays) takes ~65 ms to unmap on one thread; the commit
+// hands it to this worker instead and returns as soon as the device scene is ready.  The worker drains its
+// queue before the library unloads.  A forked child inherits the object but not the thread: it starts its
+// own and leaves the parent's alone (joining a thread of another process would hang).
+class Reaper {
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<std::shared_ptr<void>> q_;
+    bool stop_ = false;
+    std::thread* th_ = nullptr;
+    pid_t pid_ = 0;
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            std::vector<std::shared_ptr<void>> batch;
+            batch.swap(q_);
+            lk.unlock();
+            batch.clear();                              // the frees, outside the lock
+            lk.lock();
+            if (stop_ && q_.empty()) return;
+        }
+    }
+public:
+    template <class... V>
+    void reap(V&&... v) {
+        auto bundle = std::make_shared<std::tuple<std::decay_t<V>...>>(std::move(v)...);
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!th_ || pid_ != getpid()) {
+            th_ = new std::thread([this] { run(); });   // (a parent's thread object stays with the parent)
+            pid_ = getpid();
+        }
+        q_.push_back(std::move(bundle));
+        cv_.notify_one();
+    }
+    ~Reaper() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_one();
+        if (th_ && pid_ == getpid()) {
+            th_->join();
+            delete th_;
+        }
+    }
+};
+Reaper g_reaper;
 
 #ifdef RT_COMMIT_PROFILE
 #define COMMIT_MARK(tag) std::fprintf(stderr, "commit %-12s %9.1f ms\n", tag, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - cp0).count())
@@ -417,14 +477,15 @@ int commit_scene(Scene* s, int world) {
     std::vector<int> chain_order;   // -1 first
     chain_order.push_back(-1);
     for (size_t i = 0; i < f.chains.size(); ++i) chain_order.push_back((int)i);
-    std::vector<SphereRec> sph;
-    std::vector<MSphereRec> msph;
+    HostVec<SphereRec> sph;                          // (filled by threads after a resize: rt_bvh.h, NoInit)
+    HostVec<MSphereRec> msph;
     std::vector<RectRec> rect;
     std::vector<Group> groups;
-    std::vector<LeafInfo> lsph, lmsph, lrect[3];
+    HostVec<LeafInfo> lsph, lmsph;
+    std::vector<LeafInfo> lrect[3];
 
-    std::vector<BezierRec> bez;
-    std::vector<LeafInfo> lbez;
+    HostVec<BezierRec> bez;
+    HostVec<LeafInfo> lbez;
     std::vector<KleinRec> klein;
     std::vector<LeafInfo> lklein;
     auto bezier_rec = [](const Obj& o) {
@@ -499,17 +560,17 @@ int commit_scene(Scene* s, int world) {
     COMMIT_MARK("refs");
     const bool use_bvh = !refs.empty() && refs.size() >= bvh_min_prims();
     std::vector<BvhNode> bvh_nodes;
-    std::vector<BvhNode2> bvh2;
-    std::vector<BvhLeaf> bleaf;
+    HostVec<BvhNode2> bvh2;
+    HostVec<BvhLeaf> bleaf;
     int32_t bvh2_root = 0;
     int32_t lane_stack = 0;
-    std::vector<BvhNode4> bvh4;                      // curve trees (k_extend_curves)
+    HostVec<BvhNode4> bvh4;                          // curve trees (k_extend_curves)
     int32_t bvh4_root = 0, stack4 = 0;
     bool bvh_has_bez = false;
     float bvh_pad = 0.0f;
     double margin = 0.0;
-    std::vector<BvhNode2> fbvh2;                     // time-0 tree (see below)
-    std::vector<BvhLeaf> fbleaf;
+    HostVec<BvhNode2> fbvh2;                         // time-0 tree (see below)
+    HostVec<BvhLeaf> fbleaf;
     std::vector<SphereRec> fsph;
     std::vector<std::pair<int, int>> fsrc;           // (LEAF_SPHERE | LEAF_MSPHERE, local)
     int32_t fbvh2_root = 0;
@@ -538,15 +599,18 @@ int commit_scene(Scene* s, int world) {
         }
         bvh_has_bez = nb[refs.size()] > 0;
         bvh_nodes = std::move(bb.nodes);
+        COMMIT_MARK("prefix");
         // f32 box margin: 2^-21 x a radius bound R on everything a ray can start
         // from (x4 included, see scene_radius).  The slab ends carry at most
         // ~4 ulps x (|box| + |o|) <= 2^-22 x 1.25 R of rounding; the margin is
         // 1.6x that.
         margin = std::ldexp(scene_radius(s, f), -21);
         bvh_pad = (float)margin;
+        COMMIT_MARK("radius");
         flatten_bvh2(bvh_nodes, margin, [&](int b, int e) {
             return BvhLeaf{ns[b], ns[e] - ns[b], nm[b], nm[e] - nm[b], nb[b], nb[e] - nb[b], 0, 0};
         }, bvh2, bleaf, bvh2_root, lane_stack, threads);
+        COMMIT_MARK("flatten2");
         if (bvh_has_bez) {                               // single-curve leaves: direct refs (kDirectCurve)
             auto direct = [&](int32_t& ref) {
                 if (ref >= 0) return;
@@ -556,7 +620,7 @@ int commit_scene(Scene* s, int world) {
             for (BvhNode2& M : bvh2) { direct(M.l); direct(M.r); }
             direct(bvh2_root);
             COMMIT_MARK("bvh2");
-            bvh4_root = collapse_bvh4(bvh2, bvh2_root, bvh4, stack4);
+            bvh4_root = collapse_bvh4(bvh2, bvh2_root, bvh4, stack4, threads);
             COMMIT_MARK("bvh4");
         }
         groups.push_back(Group{GROUP_BVH, -1, 0, (int)bvh_nodes.size()});
@@ -565,6 +629,7 @@ int commit_scene(Scene* s, int world) {
         sph.resize((size_t)ns[refs.size()]); lsph.resize(sph.size());
         msph.resize((size_t)nm[refs.size()]); lmsph.resize(msph.size());
         bez.resize((size_t)nb[refs.size()]); lbez.resize(bez.size());
+        COMMIT_MARK("resize");
         parallel_for(refs.size(), bb.threads, [&](const size_t b, const size_t e) {
             for (size_t i = b; i < e; ++i) {
                 const PrimRef& r = refs[i];
@@ -743,6 +808,7 @@ int commit_scene(Scene* s, int world) {
             else ls.push_back(&f.leaves[i]);
         }
         emit_groups(ls, groups, true, use_bvh && sg == 0);
+        COMMIT_MARK("emit");
         if (!medium) continue;
         const Obj& o = s->objs[medium->obj];
         MediumRec m{};
@@ -764,27 +830,32 @@ int commit_scene(Scene* s, int world) {
         lrect[0].size() + lrect[1].size() + lrect[2].size() != rect.size())
         return fail("internal: leaf records and leaf infos out of step");
     // leaf ids: spheres, moving spheres, then all rects (rect locals index the shared rect array)
-    std::vector<LeafInfo> leaves;
-    leaves.reserve(lsph.size() + lmsph.size() + rect.size() + lbez.size() + lmed.size() + lklein.size());
-    int32_t base[kLeafTypes];
-    base[LEAF_SPHERE] = 0;
-    for (auto& li : lsph) leaves.push_back(li);
-    base[LEAF_MSPHERE] = (int32_t)leaves.size();
-    for (auto& li : lmsph) leaves.push_back(li);
     // rect arrays are shared between the three axis types; leaf id = rect_base + local
-    int32_t rect_base = (int32_t)leaves.size();
     std::vector<LeafInfo> rl(rect.size());
     for (int a = 0; a < 3; ++a) for (auto& li : lrect[a]) rl[li.local] = li;
-    for (auto& li : rl) leaves.push_back(li);
-    base[LEAF_RECT_XY] = base[LEAF_RECT_XZ] = base[LEAF_RECT_YZ] = rect_base;
-    base[LEAF_BEZIER] = (int32_t)leaves.size();
-    for (auto& li : lbez) leaves.push_back(li);
-    base[LEAF_MEDIUM] = (int32_t)leaves.size();
-    for (auto& li : lmed) leaves.push_back(li);
-    base[LEAF_KLEIN] = (int32_t)leaves.size();
-    for (auto& li : lklein) leaves.push_back(li);
+    int32_t base[kLeafTypes];
+    base[LEAF_SPHERE] = 0;
+    base[LEAF_MSPHERE] = base[LEAF_SPHERE] + (int32_t)lsph.size();
+    base[LEAF_RECT_XY] = base[LEAF_RECT_XZ] = base[LEAF_RECT_YZ] = base[LEAF_MSPHERE] + (int32_t)lmsph.size();
+    base[LEAF_BEZIER] = base[LEAF_RECT_XY] + (int32_t)rl.size();
+    base[LEAF_MEDIUM] = base[LEAF_BEZIER] + (int32_t)lbez.size();
+    base[LEAF_KLEIN] = base[LEAF_MEDIUM] + (int32_t)lmed.size();
+    HostVec<LeafInfo> leaves;
+    leaves.resize((size_t)base[LEAF_KLEIN] + lklein.size());
+    auto put = [&](const LeafInfo* src, const size_t n, const int32_t at) {
+        parallel_for(n, threads, [&](const size_t b, const size_t e) { std::copy(src + b, src + e, leaves.data() + at + b); });
+    };
+    put(lsph.data(), lsph.size(), base[LEAF_SPHERE]);
+    put(lmsph.data(), lmsph.size(), base[LEAF_MSPHERE]);
+    put(rl.data(), rl.size(), base[LEAF_RECT_XY]);
+    put(lbez.data(), lbez.size(), base[LEAF_BEZIER]);
+    put(lmed.data(), lmed.size(), base[LEAF_MEDIUM]);
+    put(lklein.data(), lklein.size(), base[LEAF_KLEIN]);
+    COMMIT_MARK("leaves");
     // the shade-side fields: material, texture shortcut, sphere centre (LeafInfo)
-    for (LeafInfo& li : leaves) {
+    parallel_for(leaves.size(), threads, [&](const size_t lb, const size_t le) {
+      for (size_t lk = lb; lk < le; ++lk) {
+        LeafInfo& li = leaves[lk];
         if (li.mat < 0 || li.mat >= (int)s->mats.size()) continue;     // boundary placeholders
         const DevMaterial& m = s->mats[li.mat];
         li.mtype = m.type;
@@ -812,7 +883,8 @@ int commit_scene(Scene* s, int world) {
             const double frac = (0.0 - M.t0) / M.den;
             li.c[0] = M.c0x + M.dcx * frac; li.c[1] = M.c0y + M.dcy * frac; li.c[2] = M.c0z + M.dcz * frac;
         }
-    }
+      }
+    });
 
     std::vector<Chain> chains;
     for (auto& cv : f.chains) {
@@ -968,6 +1040,9 @@ int commit_scene(Scene* s, int world) {
     COMMIT_MARK("upload");
     HIPCHK(hipMemcpy(s->d_dev.p, &d, sizeof(DevScene), hipMemcpyHostToDevice));
     s->committed = true;
+    g_reaper.reap(std::move(f), std::move(refs), std::move(bvh_nodes), std::move(bvh2), std::move(bleaf), std::move(bvh4),
+                  std::move(sph), std::move(msph), std::move(bez), std::move(lsph), std::move(lmsph), std::move(lbez),
+                  std::move(leaves), std::move(fbvh2), std::move(fbleaf), std::move(fsph));
     return 0;
 }
 
@@ -1098,6 +1173,7 @@ int lanes_for(const Context& c, const DevScene& d) {
 // 356.1, 32 spp 394.8 vs 395.8, 256 spp (128-spp chunks) 402.9 vs 407.8 — so it is taken for depth-1
 // launches of at most kFuseMaxRays rays (full frames below ~16 spp per chunk, e.g. the progressive
 // one-pass-at-a-time loop, main.scm:533-544).  RTAMD_CURVE_FUSE=0 / 1: never / always (A/B, tests).
+// (2^23 / 2^25: the same within noise at 32 and 256 spp, profiles/r06/fuse_max/)
 constexpr uint32_t kFuseMaxRays = 1u << 24;
 bool curve_fuse(const DevScene& d, const uint32_t n) {
     if (!(curve_kernel_scene(d) && curve_persistent() && !d.has_perlin && d.light.type == LIGHT_OFF)) return false;
@@ -1881,6 +1957,10 @@ int rt_scene_commit(int scene, int world) {
     const auto t0 = std::chrono::steady_clock::now();
     tl_upload_ms = 0.0;
     const int rc = commit_scene(s, world);
+#ifdef RT_COMMIT_PROFILE
+    std::fprintf(stderr, "commit %-12s %9.1f ms\n", "return",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+#endif
     s->commit_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     s->commit_upload_ms = tl_upload_ms;
     return rc;

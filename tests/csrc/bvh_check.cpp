@@ -1,7 +1,8 @@
 // bvh_check.cpp — the threaded scene-commit BVH build (scheme-raytrace_amd/csrc/rt_bvh.h, round 6: key-pair
-// sorts in the SAH sweep, subtrees on host threads) against the round-5 serial builder (RefBuild below,
-// std::stable_sort sweeps), on the host (no GPU): the same node array bit for bit, the same primitive
-// order, the same BVH2 layout and BVH4 collapse.  Input: a file of n primitives, 7 doubles each (lo[3], hi[3] of the
+// sorts in the SAH sweep, centroid orders passed down the sweep, subtrees on host threads, the BVH4 collapse
+// numbered from subtree sizes) against the round-5 serial builder (RefBuild below, std::stable_sort sweeps)
+// and its stack-order collapse (ref_collapse_bvh4), on the host (no GPU): the same node array bit for bit,
+// the same primitive order, the same BVH2 layout and BVH4 array.  Input: a file of n primitives, 7 doubles each (lo[3], hi[3] of the
 // unpadded box, type), as commit_scene forms them (curves: control points +- width/2).  Prints one JSON
 // line with both build times.  usage: bvh_check FILE THREADS [SWEEP_MAX]
 #include <chrono>
@@ -132,6 +133,58 @@ struct RefBuild {     // the round-5 builder: serial, std::stable_sort sweeps (t
     }
 };
 
+// the round-5 collapse: BVH4 nodes numbered in the order a stack of (BVH2 node, BVH4 index) pairs fills them
+static int32_t ref_collapse_bvh4(const std::vector<BvhNode2>& bvh2, int32_t root, std::vector<BvhNode4>& bvh4, int32_t& stack4) {
+    stack4 = 0;
+    if (root < 0) return root;
+    struct Slot { int32_t ref; float lo[3], hi[3]; };
+    auto child = [&](const BvhNode2& M, const int side, Slot& o) {
+        o.ref = side ? M.r : M.l;
+        for (int k = 0; k < 3; ++k) { o.lo[k] = M.b[2 * k + side]; o.hi[k] = M.b[6 + 2 * k + side]; }
+    };
+    std::vector<std::pair<int32_t, int32_t>> todo{{root, 0}};
+    std::vector<int32_t> need(1, 0), parent(1, -1);
+    bvh4.assign(1, BvhNode4{});
+    while (!todo.empty()) {
+        const auto [p, q] = todo.back();
+        todo.pop_back();
+        Slot sl[4];
+        int n = 0;
+        for (int side = 0; side < 2; ++side) {
+            Slot c;
+            child(bvh2[p], side, c);
+            if (c.ref >= 0) { child(bvh2[c.ref], 0, sl[n++]); child(bvh2[c.ref], 1, sl[n++]); }
+            else sl[n++] = c;
+        }
+        BvhNode4 N{};
+        for (int j = 0; j < 4; ++j)
+            for (int k = 0; k < 3; ++k) { N.lo[k][j] = 0.0f; N.hi[k][j] = -1.0f; }
+        N.n = n;
+        for (int j = 0; j < n; ++j) {
+            for (int k = 0; k < 3; ++k) { N.lo[k][j] = sl[j].lo[k]; N.hi[k][j] = sl[j].hi[k]; }
+            if (sl[j].ref >= 0) {
+                const int32_t q2 = (int32_t)bvh4.size();
+                bvh4.push_back(BvhNode4{});
+                need.push_back(0);
+                parent.push_back(q);
+                todo.push_back({sl[j].ref, q2});
+                N.ref[j] = q2;
+            } else {
+                N.ref[j] = sl[j].ref;
+            }
+        }
+        for (int j = n; j < 4; ++j) N.ref[j] = sl[0].ref;
+        bvh4[q] = N;
+        need[q] = n - 1;
+    }
+    std::vector<int32_t> deep(bvh4.size(), 0), below(bvh4.size(), 0);
+    for (size_t q = bvh4.size(); q-- > 0;) {
+        deep[q] = need[q] + below[q];
+        if (parent[q] >= 0) below[parent[q]] = std::max(below[parent[q]], deep[q]);
+    }
+    stack4 = deep[0];
+    return 0;
+}
 
 static std::vector<PrimRef> load(const char* path) {
     FILE* f = std::fopen(path, "rb");
@@ -170,7 +223,8 @@ static Built run(std::vector<PrimRef> refs, int threads, int sweep) {
     std::vector<BvhLeaf> bleaf;
     flatten_bvh2(o.nodes, 1e-6, [&](int b, int e) { return BvhLeaf{b, e - b, 0, 0, 0, 0, 0, 0}; }, o.bvh2, bleaf,
                  o.root, o.stack, std::is_same<B, BvhBuild>::value ? threads : 1);
-    collapse_bvh4(o.bvh2, o.root, o.bvh4, o.stack4);
+    if constexpr (std::is_same<B, BvhBuild>::value) collapse_bvh4(o.bvh2, o.root, o.bvh4, o.stack4, threads);
+    else ref_collapse_bvh4(o.bvh2, o.root, o.bvh4, o.stack4);
     return o;
 }
 

@@ -43,8 +43,11 @@ def _run(exe, boxes, path, threads, sweep=None):
 
 
 def test_threaded_curve_bvh_equals_serial(bvh_check, tmp_path):
-    res = _run(bvh_check, _curve_boxes(1 << 16, 0.5), tmp_path / "c.bin", 8)
-    assert res["same_nodes"] and res["same_order"] and res["same_bvh4"]
+    """2^17 curves: sweep levels with the centroid orders passed down, and a BVH2 large enough (>= 65 536
+    inner nodes) for the threaded BVH4 collapse."""
+    res = _run(bvh_check, _curve_boxes(1 << 17, 0.5), tmp_path / "c.bin", 8)
+    assert res["nodes"] >= 2 * 65536
+    assert res["same_nodes"] and res["same_order"] and res["same_bvh2"] and res["same_bvh4"]
 
 
 def test_threaded_build_binned_top_and_spheres(bvh_check, tmp_path):
@@ -57,4 +60,17 @@ def test_threaded_build_binned_top_and_spheres(bvh_check, tmp_path):
     r = rs.uniform(0.1, 2.0, size=(20000, 1))
     boxes = np.concatenate([c - r, c + r, np.zeros((20000, 1))], axis=1)
     res = _run(bvh_check, boxes, tmp_path / "s.bin", 3)
-    assert res["same_nodes"] and res["same_bvh2"]
+    assert res["same_nodes"] and res["same_order"] and res["same_bvh2"] and res["same_bvh4"]
+
+
+def test_sweep_orders_with_ties_below_binned_levels(bvh_check, tmp_path):
+    """Every centroid three times (ties on all axes) and centroids on a coarse grid (ties on one axis at a
+    time), binned above 4096 primitives: the sweep roots sort, their subtrees split the sorted orders and
+    re-order tied runs by position — the stable sort's order at every node."""
+    rs = np.random.default_rng(11)
+    c = np.round(rs.uniform(-40, 40, size=(50000, 3)) * 4) / 4
+    c = np.concatenate([c, c, c])
+    r = rs.uniform(0.1, 1.0, size=(150000, 1))
+    boxes = np.concatenate([c - r, c + r, np.zeros((150000, 1))], axis=1)
+    res = _run(bvh_check, boxes, tmp_path / "t.bin", 6, sweep=4096)
+    assert res["same_nodes"] and res["same_order"] and res["same_bvh2"] and res["same_bvh4"]
