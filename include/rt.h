@@ -93,13 +93,13 @@ int rt_context_release_pools(int ctx);
  *                     mixture's sphere sampler): RT_LIBM_EXACT = the reference
  *                     runtime's C library bit for bit (glibc's algorithm,
  *                     restated on the device), RT_LIBM_DEVICE = the device
- *                     library (within 1 ulp, ~4.5 % faster on the cover scene),
+ *                     library (within 1 ulp, ~1.4 % faster on the cover scene),
  *                     RT_LIBM_AUTO (0) = exact in scenes with curves (where an
  *                     ulp of a bounce direction changes which ribbon a grazing
  *                     ray hits) or noise / marble textures (C3: 0.8 % of the
  *                     horizon rows' pixels moved by > 1e-9 otherwise; exact
  *                     costs it 1.7 %), the device library elsewhere (the cover
- *                     scene: 0.3 % of those pixels, exact would cost 5.5 %).
+ *                     scene: 0.3 % of those pixels, exact would cost 1.4 %).
  *                     The marble texture's sin is exact in every mode. */
 enum { RT_OPT_LANES = 1, RT_OPT_MAX_PATHS = 2, RT_OPT_TAIL_PATHS = 3, RT_OPT_TAIL_DIV = 4, RT_OPT_TAIL_OFF = 5,
        RT_OPT_EXACT_LIBM = 6 };
