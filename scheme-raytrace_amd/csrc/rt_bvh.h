@@ -106,8 +106,6 @@ struct BvhBuild {
     static void grow(double* lo, double* hi, const double* plo, const double* phi) {
         for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], plo[k]); hi[k] = std::max(hi[k], phi[k]); }
     }
-    // One node over refs [b, e): its box, and either a leaf (returns -1; N.c = -2, N.a / N.b = the range) or a
-    // split (returns mid, refs [b, mid) / [mid, e) reordered for the children; N.c = -1, N.d = the axis).
     static bool c_same(const double x, const double y) { return !c_less(x, y) && !c_less(y, x); }
     // One node over refs [b, e): its box, and either a leaf (returns -1; N.c = -2, N.a / N.b = the range) or a
     // split (returns mid, refs [b, mid) / [mid, e) reordered for the children; N.c = -1, N.d = the axis).
@@ -316,24 +314,23 @@ inline void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafF
     const size_t nn = nodes.size();
     std::vector<int> idx(nn);
     const int nt = (threads > 1 && nn >= 65536) ? threads : 1;
-    const size_t chunk = (nn + (size_t)nt - 1) / (size_t)nt;
+    const size_t chunk = std::max<size_t>(1, (nn + (size_t)nt - 1) / (size_t)nt);
     std::vector<size_t> n_in((size_t)nt + 1, 0), n_lf((size_t)nt + 1, 0);
-    parallel_for((size_t)nt, nt, [&](const size_t tb, const size_t te) {
-        for (size_t t = tb; t < te; ++t)
-            for (size_t i = t * chunk; i < std::min(nn, (t + 1) * chunk); ++i)
-                (nodes[i].c == -1 ? n_in : n_lf)[t + 1] += 1;
+    // (parallel_for cuts [0, nn) into the same nt ranges of `chunk` nodes: range t starts at t * chunk)
+    parallel_for(nn, nt, [&](const size_t b, const size_t e) {
+        const size_t t = b / chunk;
+        for (size_t i = b; i < e; ++i) (nodes[i].c == -1 ? n_in : n_lf)[t + 1] += 1;
     });
     for (int t = 0; t < nt; ++t) { n_in[t + 1] += n_in[t]; n_lf[t + 1] += n_lf[t]; }
     const size_t in0 = bvh2.size(), lf0 = bleaf.size();
     bvh2.resize(in0 + n_in[nt]);
     bleaf.resize(lf0 + n_lf[nt]);
-    parallel_for((size_t)nt, nt, [&](const size_t tb, const size_t te) {
-        for (size_t t = tb; t < te; ++t) {
-            size_t a = in0 + n_in[t], l = lf0 + n_lf[t];
-            for (size_t i = t * chunk; i < std::min(nn, (t + 1) * chunk); ++i) {
-                if (nodes[i].c == -1) { idx[i] = (int)a; bvh2[a++] = BvhNode2{}; }
-                else { idx[i] = ~(int)l; bleaf[l++] = leaf_of(nodes[i].a, nodes[i].b); }
-            }
+    parallel_for(nn, nt, [&](const size_t b, const size_t e) {
+        const size_t t = b / chunk;
+        size_t a = in0 + n_in[t], l = lf0 + n_lf[t];
+        for (size_t i = b; i < e; ++i) {
+            if (nodes[i].c == -1) { idx[i] = (int)a; bvh2[a++] = BvhNode2{}; }
+            else { idx[i] = ~(int)l; bleaf[l++] = leaf_of(nodes[i].a, nodes[i].b); }
         }
     });
     parallel_for(nn, threads, [&](const size_t b, const size_t e) {    // each node on its own

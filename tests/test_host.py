@@ -49,7 +49,7 @@ def test_library_loads_and_reports_errors_without_gpu():
 
 
 def test_new_abi_entry_points_refuse_bad_handles_without_gpu():
-    """ABI 6 entry points check their handles and arguments before any device or RCCL call."""
+    """ABI 6 / 7 entry points check their handles and arguments before any device or RCCL call."""
     L = _lib.lib()
     h = ctypes.c_int(0)
     uid = (ctypes.c_uint8 * _lib.RT_COMM_ID_BYTES)()
@@ -63,6 +63,21 @@ def test_new_abi_entry_points_refuse_bad_handles_without_gpu():
     assert L.rt_curve_depth_probe(424242, 1, None, None, None) != 0
     assert b"invalid context" in L.rt_last_error()
     assert L.rt_context_set_option(424242, _lib.RT_OPTIONS["exact_libm"], 1) != 0
+    # ABI 7 (round 6): the host-only layout and the one-device gather
+    cnt = (ctypes.c_int64 * 4)()
+    off = (ctypes.c_int64 * 4)()
+    assert L.rt_gather_layout(0, 4, 2, cnt, off) != 0
+    assert b"positive" in L.rt_last_error()
+    assert L.rt_gather_layout(4, 4, 0, cnt, off) != 0
+    assert b"world" in L.rt_last_error()
+    assert L.rt_gather_layout(4, 4, 2, None, off) != 0
+    assert L.rt_gather_layout(1 << 16, 1 << 16, 2, cnt, off) != 0
+    assert b"too large" in L.rt_last_error()
+    bufs = (ctypes.c_void_p * 2)()
+    assert L.rt_gather_shards_local(424242, 4, 4, 2, ctypes.cast(bufs, ctypes.c_void_p), ctypes.c_void_p(16), None) != 0
+    assert b"invalid context" in L.rt_last_error()
+    assert L.rt_gather_shards_local(424242, 4, 4, 2, None, ctypes.c_void_p(16), None) != 0
+    assert b"null" in L.rt_last_error()
 
 
 def test_random_scene_structure():
