@@ -471,6 +471,7 @@ int commit_scene(Scene* s, int world) {
         if ((t.type == TEX_NOISE || t.type == TEX_MARBLE) && !s->have_perlin)
             return fail("rt_scene_commit: noise/marble texture needs rt_set_perlin_tables");
     Flattener f{s};
+    f.leaves.reserve(s->objs.size());                // (a hint: an object listed twice is two leaves)
     if (int rc = f.walk(world, 0)) return rc;
 
     // group leaves by (chain, type) in first-appearance order of chains

@@ -318,8 +318,10 @@ inline void flatten_bvh2(const std::vector<BvhNode>& nodes, double margin, LeafF
     std::vector<size_t> n_in((size_t)nt + 1, 0), n_lf((size_t)nt + 1, 0);
     // (parallel_for cuts [0, nn) into the same nt ranges of `chunk` nodes: range t starts at t * chunk)
     parallel_for(nn, nt, [&](const size_t b, const size_t e) {
-        const size_t t = b / chunk;
-        for (size_t i = b; i < e; ++i) (nodes[i].c == -1 ? n_in : n_lf)[t + 1] += 1;
+        size_t ni = 0;                                 // (counted locally: the shared counts sit on one line)
+        for (size_t i = b; i < e; ++i) ni += nodes[i].c == -1;
+        n_in[b / chunk + 1] = ni;
+        n_lf[b / chunk + 1] = (e - b) - ni;
     });
     for (int t = 0; t < nt; ++t) { n_in[t + 1] += n_in[t]; n_lf[t + 1] += n_lf[t]; }
     const size_t in0 = bvh2.size(), lf0 = bleaf.size();
