@@ -43,9 +43,9 @@ def _run(exe, boxes, path, threads, sweep=None):
 
 
 def test_threaded_curve_bvh_equals_serial(bvh_check, tmp_path):
-    """2^17 curves: sweep levels with the centroid orders passed down, and a BVH2 large enough (>= 65 536
-    inner nodes) for the threaded BVH4 collapse."""
-    res = _run(bvh_check, _curve_boxes(1 << 17, 0.5), tmp_path / "c.bin", 8)
+    """2^18 curves: binned top levels over sweep levels with the centroid orders passed down, and a BVH2
+    large enough (>= 65 536 inner nodes) for the threaded BVH4 collapse."""
+    res = _run(bvh_check, _curve_boxes(1 << 18, 0.5), tmp_path / "c.bin", 8)
     assert res["nodes"] >= 2 * 65536
     assert res["same_nodes"] and res["same_order"] and res["same_bvh2"] and res["same_bvh4"]
 
